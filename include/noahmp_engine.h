@@ -1,0 +1,229 @@
+/*
+ * noahmp_engine.h -- C ABI of the MI355X Noah-MP column engine.
+ *
+ * Drop-in for the reference engine slot `module noahmp_engine`
+ * (/root/reference/core/module_noahmp_engine.f90:5-10: empty `noahmp_init`,
+ * `noahmp_run`) and for the per-column physics entry it was meant to drive,
+ * `noahmp_sflx` (core/module_noahmp_func.f90:66-91, 131 by-reference args).
+ *
+ * Entry point                 replaces (reference file:line)
+ * --------------------------  ------------------------------------------------
+ * nmp_read_tables             noahmp_gen_param_readptable   core/module_noahmp_gen_param.f90:51-89
+ *                             noahmp_soil_param_readptable  core/module_noahmp_soil_param.f90:31-72
+ *                             noahmp_veg_param_readptable   core/module_noahmp_veg_param.f90:77-161
+ *                             (block/tag finder             core/module_noahmp_utils.f90:200-237)
+ * nmp_init                    noahmp_init                   core/module_noahmp_engine.f90:5-6
+ *                             noahmp_set_options            core/module_noahmp_global.f90:77-112
+ * nmp_step                    noahmp_run                    core/module_noahmp_engine.f90:8-10
+ *                             = noahmp_sflx over every column core/module_noahmp_func.f90:66-476
+ * nmp_state_from_aos          layout bridge from noahmp_state_t records
+ *                                                           core/module_noahmp_type.f90:10-42
+ * nmp_finalize, nmp_strerror  (error path of utils `assert`/`stop`, core/module_noahmp_utils.f90:21-53)
+ *
+ * Conventions
+ *  - Plain pointers and sizes only.  All per-column arrays are structure of
+ *    arrays, field-major: field f of column c lives at base[f*ld + c]
+ *    (ld >= ncol), so one wavefront of 64 lanes reads 64 consecutive columns
+ *    of one field per load.
+ *  - "real" arrays are float when the engine was created with precision 4 and
+ *    double with precision 8.  Table values (nmp_params) are always float, as
+ *    in the reference (real(r4) module arrays).
+ *  - Pointers passed to nmp_step are DEVICE pointers on the engine's device;
+ *    `stream` is a hipStream_t (NULL = default stream).  nmp_step only
+ *    enqueues work; it never synchronises and never allocates.
+ *  - Return codes: 0 ok, negative = NMP_E_*.  Per-column physics failures
+ *    that abort the reference (wrf_error_fatal) are reported as NMP_ST_* bits
+ *    in col_status instead; the column continues, as the reference code does
+ *    after the external returns.
+ *  - Threading: one engine per device; calls on one engine are serialised by
+ *    the caller.  Engines on different devices/ranks are independent.
+ */
+#ifndef NOAHMP_ENGINE_H
+#define NOAHMP_ENGINE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define NMP_ABI_VERSION 1
+
+/* ---- dimensions (core/module_noahmp_global.f90:9-13) -------------------- */
+#define NMP_NSOIL 4
+#define NMP_NSNOW 3
+#define NMP_NLAYER 7 /* -NSNOW+1 .. NSOIL ; C index k <-> Fortran index k-2 */
+#define NMP_NBAND 2
+
+/* ---- physics options, order = noahmp_set_options (global.f90:77-80) ----- */
+typedef struct nmp_options {
+  int32_t opt_veg, opt_crs, opt_btr, opt_run, opt_sfc, opt_frz;
+  int32_t opt_inf, opt_rad, opt_alb, opt_snf, opt_tbot, opt_stc;
+} nmp_options;
+
+/* ---- lookup tables: the reference module arrays, in memory ------------- *
+ * Field order == the reference module declarations; 2-D Fortran arrays
+ * (band,type) / (month,type) map to C [type][band] / [type][month].
+ * Indices are 1-based in the reference: entry i of the C arrays is type i+1. */
+#define NMP_MSLOPETYP 30 /* gen_param.f90:8   */
+#define NMP_MSLTYP 30    /* soil_param.f90:7  */
+#define NMP_MSLCOL 20    /* soil_param.f90:8  */
+#define NMP_MLUTYP 27    /* veg_param.f90:8   */
+
+typedef struct nmp_params {
+  /* GENPARMMP.TBL  (gen_param.f90:12-48) */
+  float slope[NMP_MSLOPETYP];
+  float csoil, zbot, czil, dkref, kdtref, frzk, timean, fsatmax;
+  float mltfct, z0sno, ssi, swemax;
+  float albice[2], alblake[2], omegas[2];
+  float betads, betais, emssoil, emslake;
+  /* SOILPARMMP.TBL  (soil_param.f90:13-28) */
+  float bexp[NMP_MSLTYP], smcmax[NMP_MSLTYP], smcref[NMP_MSLTYP], smcwlt[NMP_MSLTYP];
+  float psisat[NMP_MSLTYP], dksat[NMP_MSLTYP], dwsat[NMP_MSLTYP], quartz[NMP_MSLTYP];
+  float kdt[NMP_MSLTYP], frzx[NMP_MSLTYP];
+  float albsat[NMP_MSLCOL][2], albdry[NMP_MSLCOL][2];
+  /* VEGPARMMP.TBL  (veg_param.f90:19-74) */
+  float xl[NMP_MLUTYP];
+  float rhol[NMP_MLUTYP][2], rhos[NMP_MLUTYP][2], taul[NMP_MLUTYP][2], taus[NMP_MLUTYP][2];
+  float canwmxp[NMP_MLUTYP], dleaf[NMP_MLUTYP], z0mvt[NMP_MLUTYP], hvt[NMP_MLUTYP];
+  float hvb[NMP_MLUTYP], den[NMP_MLUTYP], rcrown[NMP_MLUTYP], cwpvt[NMP_MLUTYP];
+  float sai12m[NMP_MLUTYP][12], lai12m[NMP_MLUTYP][12];
+  float sla[NMP_MLUTYP], dilefc[NMP_MLUTYP], dilefw[NMP_MLUTYP], fragr[NMP_MLUTYP];
+  float ltovrc[NMP_MLUTYP], wrrat[NMP_MLUTYP], wdpool[NMP_MLUTYP], tdlef[NMP_MLUTYP];
+  float rgl[NMP_MLUTYP], hs[NMP_MLUTYP], rsmax[NMP_MLUTYP], rsmin[NMP_MLUTYP], topt[NMP_MLUTYP];
+  float kc25[NMP_MLUTYP], akc[NMP_MLUTYP], ko25[NMP_MLUTYP], ako[NMP_MLUTYP];
+  float vcmx25[NMP_MLUTYP], avcmx[NMP_MLUTYP], bp[NMP_MLUTYP], mp[NMP_MLUTYP];
+  float qe25[NMP_MLUTYP], aqe[NMP_MLUTYP], folnmx[NMP_MLUTYP], tmin[NMP_MLUTYP];
+  float rmf25[NMP_MLUTYP], rms25[NMP_MLUTYP], rmr25[NMP_MLUTYP], arm[NMP_MLUTYP], mrp[NMP_MLUTYP];
+  float slarea[NMP_MLUTYP], eps[NMP_MLUTYP][5];
+  /* integers */
+  int32_t nslptyp, nsltyp, nsoilcol, nlutyp;
+  int32_t isurban, iswater, isbarren, isice, isegblf; /* veg_param.f90:13-17 */
+  int32_t nroot[NMP_MLUTYP], c3c4[NMP_MLUTYP];
+} nmp_params;
+
+/* ---- per-column SoA layouts ---------------------------------------------
+ * Prognostic fp state (read + written every step).  The first block keeps
+ * the snow/soil arrays; index k of a 7-layer field is Fortran layer k-2. */
+enum {
+  NMP_S_STC = 0,     /* [7] snow/soil temperature (K)              */
+  NMP_S_ZSNSO = 7,   /* [7] layer-bottom depth from snow surface (m, <0) */
+  NMP_S_SNICE = 14,  /* [3] snow layer ice (mm)                    */
+  NMP_S_SNLIQ = 17,  /* [3] snow layer liquid (mm)                 */
+  NMP_S_SH2O = 20,   /* [4] soil liquid water (m3/m3) ("soilwat")  */
+  NMP_S_SMC = 24,    /* [4] soil total water (m3/m3)               */
+  NMP_S_TV = 28, NMP_S_TG, NMP_S_TAH, NMP_S_EAH, NMP_S_FWET, NMP_S_CANLIQ,
+  NMP_S_CANICE, NMP_S_QSFC, NMP_S_SNOWH, NMP_S_SNEQV, NMP_S_SNEQVO, NMP_S_ALBOLD,
+  NMP_S_TAUSS, NMP_S_QSNOW, NMP_S_ZWT, NMP_S_WA, NMP_S_WT, NMP_S_WSLAKE,
+  NMP_S_LAI, NMP_S_SAI, NMP_S_LFMASS, NMP_S_RTMASS, NMP_S_STMASS, NMP_S_WOOD,
+  NMP_S_STBLCP, NMP_S_FASTCP, NMP_S_CM, NMP_S_CH,
+  NMP_NSTATE = 56 /* + int32 ISNOW in its own array */
+};
+
+/* Static fp / int per column (read every step). */
+enum { NMP_F_LAT = 0, NMP_F_ZLVL, NMP_F_SHDFAC, NMP_F_SHDMAX, NMP_F_TBOT, NMP_F_FOLN, NMP_NSTATIC_F };
+enum { NMP_I_VEGTYP = 0, NMP_I_SOILTYP, NMP_I_SLOPETYP, NMP_I_SOILCOLOR, NMP_I_IST, NMP_I_ICE,
+       NMP_NSTATIC_I };
+
+/* Forcing per step (noahmp_sflx :72-74). */
+enum { NMP_A_SFCTMP = 0, NMP_A_SFCPRS, NMP_A_PSFC, NMP_A_UU, NMP_A_VV, NMP_A_Q2, NMP_A_SOLDN,
+       NMP_A_LWDN, NMP_A_PRCP, NMP_A_COSZ, NMP_A_CO2AIR, NMP_A_O2AIR, NMP_NFORCING };
+
+/* Full diagnostics = the 58 intent(out) args of noahmp_sflx in dummy order (:82-91). */
+enum {
+  NMP_D_FSA = 0, NMP_D_FSR, NMP_D_FIRA, NMP_D_FSH, NMP_D_SSOIL, NMP_D_FCEV,
+  NMP_D_FGEV, NMP_D_FCTR, NMP_D_ECAN, NMP_D_ETRAN, NMP_D_EDIR, NMP_D_TRAD,
+  NMP_D_TGB, NMP_D_TGV, NMP_D_T2MV, NMP_D_T2MB, NMP_D_Q2V, NMP_D_Q2B,
+  NMP_D_RUNSRF, NMP_D_RUNSUB, NMP_D_APAR, NMP_D_PSN, NMP_D_SAV, NMP_D_SAG,
+  NMP_D_FSNO, NMP_D_NEE, NMP_D_GPP, NMP_D_NPP, NMP_D_FVEG, NMP_D_ALBEDO,
+  NMP_D_QSNBOT, NMP_D_PONDING, NMP_D_PONDING1, NMP_D_PONDING2, NMP_D_RSSUN, NMP_D_RSSHA,
+  NMP_D_BGAP, NMP_D_WGAP, NMP_D_CHV, NMP_D_CHB, NMP_D_EMISSI,
+  NMP_D_SHG, NMP_D_SHC, NMP_D_SHB, NMP_D_EVG, NMP_D_EVB, NMP_D_GHV,
+  NMP_D_GHB, NMP_D_IRG, NMP_D_IRC, NMP_D_IRB, NMP_D_TR, NMP_D_EVC,
+  NMP_D_CHLEAF, NMP_D_CHUC, NMP_D_CHV2, NMP_D_CHB2, NMP_D_FPICE,
+  NMP_NDIAG_FULL = 58
+};
+
+/* Output-step surface fluxes, gathered across ranks at output steps. */
+enum {
+  NMP_O_FSA = 0, NMP_O_FSR, NMP_O_FIRA, NMP_O_FSH, NMP_O_SSOIL, NMP_O_FCEV, NMP_O_FGEV,
+  NMP_O_FCTR, NMP_O_ECAN, NMP_O_ETRAN, NMP_O_EDIR, NMP_O_TRAD, NMP_O_RUNSRF, NMP_O_RUNSUB,
+  NMP_O_T2M, NMP_O_ALBEDO, NMP_NDIAG_OUT = 16
+};
+
+/* diag_level for nmp_step */
+enum { NMP_DIAG_NONE = 0, NMP_DIAG_OUT = 1, NMP_DIAG_FULL = 2 };
+
+/* Per-column status bits (replace wrf_error_fatal / wrf_message). */
+enum {
+  NMP_ST_ERRSW = 1,   /* |SWDOWN-(FSA+FSR)| > 0.01     func.f90:688-710 */
+  NMP_ST_ERRENG = 2,  /* |energy residual| > 0.01 W/m2 func.f90:712-721 */
+  NMP_ST_FIRE = 4,    /* emitted longwave <= 0         func.f90:1284-1292 */
+  NMP_ST_HCAN = 8,    /* HCAN <= ZPD                   func.f90:2726-2738 */
+  NMP_ST_ZLVL = 16,   /* ZLVL <= ZPD                   func.f90:3412-3415 */
+  NMP_ST_FLERCH = 32, /* Flerchinger fallback (info)   func.f90:4588-4590 */
+  NMP_ST_OPTVEG = 64, /* unknown opt_veg               func.f90:375-377 */
+  NMP_ST_STOP = 128   /* FIRE|ZLVL as the reference oracle reports them (one message) */
+};
+
+/* ---- errors -------------------------------------------------------------- */
+enum {
+  NMP_OK = 0,
+  NMP_E_ARG = -1,      /* bad argument / null pointer / ld < ncol          */
+  NMP_E_TABLE = -2,    /* table file missing, block not found, parse error */
+  NMP_E_OPTION = -3,   /* option value outside the reference's range      */
+  NMP_E_DEVICE = -4,   /* HIP error (no device, launch failure)           */
+  NMP_E_PRECISION = -5 /* precision not 4 or 8                            */
+};
+
+typedef struct nmp_engine nmp_engine;
+
+/* Parse GENPARMMP.TBL / SOILPARMMP.TBL / VEGPARMMP.TBL from tbl_dir with the
+ * reference's block/tag rules ("&NAME" or "&NAME#TAG").  soil_tag is e.g.
+ * "STAS" or "STAS-RUC", veg_tag "USGS" or "MODIFIED_IGBP_MODIS_NOAH".  Every
+ * field not present in the tables is NaN, as in the reference (nan4 init). */
+int nmp_read_tables(const char* tbl_dir, const char* soil_tag, const char* veg_tag,
+                    nmp_params* out);
+
+/* Create an engine on HIP device `device` computing in `precision` (4|8)
+ * bytes.  Copies the tables to the device once. */
+int nmp_init(const nmp_params* params, const nmp_options* opts, int device, int precision,
+             nmp_engine** out);
+
+/* One noahmp_sflx time step for ncol columns (all pointers device, SoA with
+ * leading dimension ld).  zsoil[4] (<0, m) and dt are domain-wide; julian /
+ * yearlen are the step's calendar position (noahmp_sflx :67).  FICEOLD is
+ * derived on device from SNICE/SNLIQ at step start, as an offline driver does.
+ * diag may be NULL when diag_level == NMP_DIAG_NONE; col_status is OR-ed
+ * (caller zeroes it when it wants a fresh mask). */
+int nmp_step(nmp_engine* eng, int64_t ncol, int64_t ld, const float zsoil[4], float dt,
+             float julian, int32_t yearlen, void* state, int32_t* isnow, const void* static_f,
+             const int32_t* static_i, const void* forcing, void* diag, int diag_level,
+             int32_t* col_status, void* stream);
+
+/* Same step, many times: nsteps steps whose forcing slices are
+ * forcing + s*forcing_stride (elements, real type), julian advancing by
+ * dt/86400 per step.  diag (if non-NULL) receives the last step only. */
+int nmp_run(nmp_engine* eng, int64_t ncol, int64_t ld, const float zsoil[4], float dt,
+            float julian0, int32_t yearlen, int32_t nsteps, void* state, int32_t* isnow,
+            const void* static_f, const int32_t* static_i, const void* forcing,
+            int64_t forcing_stride, int32_t forcing_period, void* diag, int diag_level,
+            int32_t* col_status, void* stream);
+
+/* Host-side converter: n byte-identical `noahmp_state_t` sequence records
+ * (168 B each, core/module_noahmp_type.f90:10-42) -> host SoA float state
+ * (ld >= n) + isnow, applying the unit/sign mapping of SURVEY.md 8b.
+ * Fields the record lacks are left untouched. */
+int nmp_state_from_aos(const void* records, int64_t n, int64_t ld, float* state, int32_t* isnow,
+                       int32_t* static_i);
+
+int nmp_engine_info(const nmp_engine* eng, int* device, int* precision, nmp_options* opts);
+void nmp_finalize(nmp_engine* eng);
+const char* nmp_strerror(int code);
+int nmp_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* NOAHMP_ENGINE_H */

@@ -1,0 +1,94 @@
+"""ORACLE TEST INFRASTRUCTURE -- NOT PART OF THE PRODUCT.
+
+ctypes driver for the plain-C restatement (oracle/noahmp_oracle.c), built as
+build/liboracle_f32.so and build/liboracle_f64.so by oracle/Makefile.
+Same SoA interface as oracle/ref.py.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+from ref import PARAM_FLOAT_FIELDS, PARAM_INT_FIELDS, PARAM_SHAPES, NPARAM_F, NPARAM_I
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIBS = {4: os.path.join(HERE, "build", "liboracle_f32.so"),
+        8: os.path.join(HERE, "build", "liboracle_f64.so")}
+NST, NSF, NSI, NFC, NDG = 56, 6, 6, 12, 58
+_libs = {}
+
+
+def available(precision: int = 4) -> bool:
+    return os.path.exists(LIBS[precision])
+
+
+def pack_params(P: dict) -> bytes:
+    """dict (ref.dump_params() layout) -> bytes of `struct nmp_params`."""
+    fl = []
+    for name, w in PARAM_FLOAT_FIELDS:
+        a = np.asarray(P[name], np.float32).reshape(-1)
+        assert a.size == w, (name, a.size, w)
+        fl.append(a)
+    il = []
+    for name, w in PARAM_INT_FIELDS:
+        a = np.asarray(P[name], np.int32).reshape(-1)
+        assert a.size == w, (name, a.size, w)
+        il.append(a)
+    return np.concatenate(fl).tobytes() + np.concatenate(il).tobytes()
+
+
+def _lib(precision):
+    if precision not in _libs:
+        if not available(precision):
+            raise FileNotFoundError(f"{LIBS[precision]} missing (run make -C oracle port)")
+        lib = C.CDLL(LIBS[precision])
+        rt = np.float32 if precision == 4 else np.float64
+        rp = np.ctypeslib.ndpointer(rt, flags="C_CONTIGUOUS")
+        ip = np.ctypeslib.ndpointer(np.int32, flags="C_CONTIGUOUS")
+        creal = C.c_float if precision == 4 else C.c_double
+        lib.oracle_sflx_batch.argtypes = [C.c_int32, creal, C.c_int32, creal, rp, rp, ip, rp, ip,
+                                          rp, rp, ip, C.c_char_p, C.c_void_p]
+        lib.oracle_sflx_run.argtypes = [C.c_int32, C.c_int32, creal, C.c_int32, creal, rp, rp, ip,
+                                        rp, ip, rp, C.c_int32, rp, ip, C.c_char_p, C.c_void_p]
+        assert lib.oracle_real_bytes() == precision
+        _libs[precision] = (lib, rt)
+    return _libs[precision]
+
+
+def step(P: dict, options, zsoil, dt, yearlen, julian, state, isnow, static_f, static_i, forcing,
+         precision: int = 4):
+    """One step of the C restatement.  SoA in, SoA out: (state', isnow', diag(58,n), status)."""
+    lib, rt = _lib(precision)
+    n = isnow.shape[0]
+    st = np.ascontiguousarray(np.asarray(state, rt).T)
+    isn = np.ascontiguousarray(isnow, np.int32).copy()
+    sf = np.ascontiguousarray(np.asarray(static_f, rt).T)
+    si = np.ascontiguousarray(np.asarray(static_i, np.int32).T)
+    fc = np.ascontiguousarray(np.asarray(forcing, rt).T)
+    dg = np.zeros((n, NDG), rt)
+    status = np.zeros(n, np.int32)
+    opts = (C.c_int32 * 12)(*[int(x) for x in options])
+    lib.oracle_sflx_batch(n, dt, int(yearlen), julian, np.ascontiguousarray(zsoil, rt), st, isn, sf,
+                          si, fc, dg, status, pack_params(P), C.addressof(opts))
+    return st.T.copy(), isn, dg.T.copy(), status
+
+
+def run(P: dict, options, zsoil, dt, yearlen, julian0, state, isnow, static_f, static_i,
+        forcings, nsteps: int, precision: int = 4):
+    """nsteps steps over a forcing cycle forcings[(period, 12, n)] (timed CPU baseline)."""
+    lib, rt = _lib(precision)
+    n = isnow.shape[0]
+    st = np.ascontiguousarray(np.asarray(state, rt).T)
+    isn = np.ascontiguousarray(isnow, np.int32).copy()
+    sf = np.ascontiguousarray(np.asarray(static_f, rt).T)
+    si = np.ascontiguousarray(np.asarray(static_i, np.int32).T)
+    fc = np.ascontiguousarray(np.asarray(forcings, rt).transpose(0, 2, 1))
+    dg = np.zeros((n, NDG), rt)
+    status = np.zeros(n, np.int32)
+    opts = (C.c_int32 * 12)(*[int(x) for x in options])
+    lib.oracle_sflx_run(n, nsteps, dt, int(yearlen), julian0, np.ascontiguousarray(zsoil, rt), st,
+                        isn, sf, si, fc, fc.shape[0], dg, status, pack_params(P),
+                        C.addressof(opts))
+    return st.T.copy(), isn, dg.T.copy(), status
