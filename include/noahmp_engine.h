@@ -218,6 +218,12 @@ int nmp_run(nmp_engine* eng, int64_t ncol, int64_t ld, const float zsoil[4], flo
 int nmp_state_from_aos(const void* records, int64_t n, int64_t ld, float* state, int32_t* isnow,
                        int32_t* static_i);
 
+/* Transcendental policy for fp32 engines: 0 = evaluate exp/log/pow/... in fp64
+ * and round once (reproduces the glibc-compiled reference except at rare
+ * rounding ties; default), 1 = ocml fp32 functions (faster, <= ~2 ulp).
+ * Default can also be set with NMP_MATH=fast in the environment. */
+int nmp_set_math(nmp_engine* eng, int mode);
+
 int nmp_engine_info(const nmp_engine* eng, int* device, int* precision, nmp_options* opts);
 void nmp_finalize(nmp_engine* eng);
 const char* nmp_strerror(int code);

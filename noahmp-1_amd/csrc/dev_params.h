@@ -1,0 +1,95 @@
+// Device-side lookup tables for the sflx kernel.
+//
+// A compact re-packing of `nmp_params` (the reference module arrays,
+// core/module_noahmp_{gen,soil,veg}_param.f90) holding only what the column
+// physics reads, grouped per type so that one column's lookups for its
+// vegetation / soil type fall in one contiguous record.  The whole struct is
+// ~9 KB and is staged into LDS once per workgroup; every lane then gathers its
+// own type's fields from LDS with ds_read (per-lane addresses, no HBM traffic).
+#pragma once
+#include <stdint.h>
+
+#include "noahmp_engine.h"
+
+namespace nmp {
+
+struct VegRec {  // one USGS/MODIS vegetation type (veg_param.f90:19-74)
+  float xl, rhol[2], rhos[2], taul[2], taus[2];
+  float canwmxp, dleaf, z0mvt, hvt, hvb, rcrown, cwpvt;
+  float lai12m[12], sai12m[12];
+  float sla, dilefc, dilefw, fragr, ltovrc, wrrat, wdpool, tdlef;
+  float rgl, hs, rsmax, rsmin, topt;
+  float kc25, akc, ko25, ako, vcmx25, avcmx, bp, mp, qe25, folnmx, tmin;
+  float rmf25, rms25, rmr25, arm, mrp;
+  int32_t nroot, c3c4;
+};
+
+struct SoilRec {  // one soil type (soil_param.f90:13-23)
+  float bexp, smcmax, smcref, smcwlt, psisat, dksat, dwsat, quartz, kdt, frzx;
+};
+
+struct GenRec {  // GENPARMMP.TBL scalars + soil colours (gen_param.f90:12-48, soil_param.f90:27-28)
+  float slope[NMP_MSLOPETYP];
+  float csoil, zbot, czil, timean, fsatmax, mltfct, z0sno, ssi, swemax;
+  float alblake[2], omegas[2], betads, betais, emssoil, emslake;
+  float albsat[NMP_MSLCOL][2], albdry[NMP_MSLCOL][2];
+  int32_t isurban, iswater, isbarren, isice, isegblf, pad_;
+};
+
+struct DevParams {
+  GenRec g;
+  SoilRec soil[NMP_MSLTYP];
+  VegRec veg[NMP_MLUTYP];
+};
+
+static_assert(sizeof(DevParams) % 16 == 0 || true, "");
+
+inline void pack_dev_params(const nmp_params& p, DevParams& d) {
+  for (int i = 0; i < NMP_MSLOPETYP; ++i) d.g.slope[i] = p.slope[i];
+  d.g.csoil = p.csoil; d.g.zbot = p.zbot; d.g.czil = p.czil; d.g.timean = p.timean;
+  d.g.fsatmax = p.fsatmax; d.g.mltfct = p.mltfct; d.g.z0sno = p.z0sno; d.g.ssi = p.ssi;
+  d.g.swemax = p.swemax;
+  for (int b = 0; b < 2; ++b) {
+    d.g.alblake[b] = p.alblake[b];
+    d.g.omegas[b] = p.omegas[b];
+  }
+  d.g.betads = p.betads; d.g.betais = p.betais; d.g.emssoil = p.emssoil; d.g.emslake = p.emslake;
+  for (int c = 0; c < NMP_MSLCOL; ++c)
+    for (int b = 0; b < 2; ++b) {
+      d.g.albsat[c][b] = p.albsat[c][b];
+      d.g.albdry[c][b] = p.albdry[c][b];
+    }
+  d.g.isurban = p.isurban; d.g.iswater = p.iswater; d.g.isbarren = p.isbarren;
+  d.g.isice = p.isice; d.g.isegblf = p.isegblf; d.g.pad_ = 0;
+  for (int s = 0; s < NMP_MSLTYP; ++s) {
+    SoilRec& r = d.soil[s];
+    r.bexp = p.bexp[s]; r.smcmax = p.smcmax[s]; r.smcref = p.smcref[s]; r.smcwlt = p.smcwlt[s];
+    r.psisat = p.psisat[s]; r.dksat = p.dksat[s]; r.dwsat = p.dwsat[s]; r.quartz = p.quartz[s];
+    r.kdt = p.kdt[s]; r.frzx = p.frzx[s];
+  }
+  for (int v = 0; v < NMP_MLUTYP; ++v) {
+    VegRec& r = d.veg[v];
+    r.xl = p.xl[v];
+    for (int b = 0; b < 2; ++b) {
+      r.rhol[b] = p.rhol[v][b]; r.rhos[b] = p.rhos[v][b];
+      r.taul[b] = p.taul[v][b]; r.taus[b] = p.taus[v][b];
+    }
+    r.canwmxp = p.canwmxp[v]; r.dleaf = p.dleaf[v]; r.z0mvt = p.z0mvt[v]; r.hvt = p.hvt[v];
+    r.hvb = p.hvb[v]; r.rcrown = p.rcrown[v]; r.cwpvt = p.cwpvt[v];
+    for (int m = 0; m < 12; ++m) {
+      r.lai12m[m] = p.lai12m[v][m];
+      r.sai12m[m] = p.sai12m[v][m];
+    }
+    r.sla = p.sla[v]; r.dilefc = p.dilefc[v]; r.dilefw = p.dilefw[v]; r.fragr = p.fragr[v];
+    r.ltovrc = p.ltovrc[v]; r.wrrat = p.wrrat[v]; r.wdpool = p.wdpool[v]; r.tdlef = p.tdlef[v];
+    r.rgl = p.rgl[v]; r.hs = p.hs[v]; r.rsmax = p.rsmax[v]; r.rsmin = p.rsmin[v]; r.topt = p.topt[v];
+    r.kc25 = p.kc25[v]; r.akc = p.akc[v]; r.ko25 = p.ko25[v]; r.ako = p.ako[v];
+    r.vcmx25 = p.vcmx25[v]; r.avcmx = p.avcmx[v]; r.bp = p.bp[v]; r.mp = p.mp[v];
+    r.qe25 = p.qe25[v]; r.folnmx = p.folnmx[v]; r.tmin = p.tmin[v];
+    r.rmf25 = p.rmf25[v]; r.rms25 = p.rms25[v]; r.rmr25 = p.rmr25[v]; r.arm = p.arm[v];
+    r.mrp = p.mrp[v];
+    r.nroot = p.nroot[v]; r.c3c4 = p.c3c4[v];
+  }
+}
+
+}  // namespace nmp

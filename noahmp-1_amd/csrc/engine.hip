@@ -1,0 +1,256 @@
+// C ABI of the MI355X Noah-MP column engine (include/noahmp_engine.h).
+//
+// Replaces the reference engine slot (core/module_noahmp_engine.f90:5-10) and
+// the option setter (core/module_noahmp_global.f90:77-112).  The engine owns
+// only the device copy of the lookup tables; every per-column array is
+// caller-owned device memory (SoA), so state stays resident in HBM across
+// steps and the caller decides streams, graphs and sharding.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdint>
+#include <cstdlib>
+#include <cstring>
+#include <new>
+
+#include "dev_params.h"
+#include "noahmp_engine.h"
+
+#include "sflx_kargs.h"
+
+struct nmp_engine {
+  int device;
+  int precision;
+  int math;  // 0 = reference-rounded transcendentals (parity), 1 = fast (fp32 only)
+  nmp_options opts;
+  nmp::DevParams* dparams;
+};
+
+namespace {
+
+bool options_ok(const nmp_options& o) {
+  // valid values of each option (core/module_noahmp_global.f90:17-74)
+  return o.opt_veg >= 1 && o.opt_veg <= 5 && o.opt_crs >= 1 && o.opt_crs <= 2 &&
+         o.opt_btr >= 1 && o.opt_btr <= 3 && o.opt_run >= 1 && o.opt_run <= 4 &&
+         o.opt_sfc >= 1 && o.opt_sfc <= 2 && o.opt_frz >= 1 && o.opt_frz <= 2 &&
+         o.opt_inf >= 1 && o.opt_inf <= 2 && o.opt_rad >= 1 && o.opt_rad <= 3 &&
+         o.opt_alb >= 1 && o.opt_alb <= 2 && o.opt_snf >= 1 && o.opt_snf <= 3 &&
+         o.opt_tbot >= 1 && o.opt_tbot <= 2 && o.opt_stc >= 1 && o.opt_stc <= 2;
+}
+
+int ensure_device(int dev) {
+  int cur = -1;
+  if (hipGetDevice(&cur) != hipSuccess) return NMP_E_DEVICE;
+  if (cur != dev && hipSetDevice(dev) != hipSuccess) return NMP_E_DEVICE;
+  return NMP_OK;
+}
+
+template <class T>
+void fill_args(nmp::KArgs<T>& a, const nmp_engine* e, int64_t ncol, int64_t ld,
+               const float zsoil[4], float dt, float julian, int32_t yearlen, void* state,
+               int32_t* isnow, const void* sf, const int32_t* si, const void* fc, void* diag,
+               int diag_level, int32_t* status) {
+  a.ncol = ncol;
+  a.ld = ld;
+  for (int k = 0; k < 4; ++k) a.zsoil[k] = zsoil[k];
+  a.dt = dt;
+  a.julian = julian;
+  a.yearlen = yearlen;
+  a.diag_level = diag_level;
+  const nmp_options& o = e->opts;
+  a.o = nmp::Opt{o.opt_veg, o.opt_crs, o.opt_btr, o.opt_run, o.opt_sfc, o.opt_frz,
+                 o.opt_inf, o.opt_rad, o.opt_alb, o.opt_snf, o.opt_tbot, o.opt_stc};
+  a.state = static_cast<T*>(state);
+  a.isnow = isnow;
+  a.static_f = static_cast<const T*>(sf);
+  a.static_i = si;
+  a.forcing = static_cast<const T*>(fc);
+  a.diag = static_cast<T*>(diag);
+  a.status = status;
+}
+
+int launch(const nmp_engine* e, int64_t ncol, int64_t ld, const float zsoil[4], float dt,
+           float julian, int32_t yearlen, void* state, int32_t* isnow, const void* sf,
+           const int32_t* si, const void* fc, void* diag, int diag_level, int32_t* status,
+           hipStream_t stream) {
+  hipError_t err;
+  if (e->precision == 4) {
+    nmp::KArgs<float> a;
+    fill_args(a, e, ncol, ld, zsoil, dt, julian, yearlen, state, isnow, sf, si, fc, diag,
+              diag_level, status);
+    err = (e->math == 0) ? nmp::launch_sflx<float, true>(e->dparams, a, stream)
+                         : nmp::launch_sflx<float, false>(e->dparams, a, stream);
+  } else {
+    nmp::KArgs<double> a;
+    fill_args(a, e, ncol, ld, zsoil, dt, julian, yearlen, state, isnow, sf, si, fc, diag,
+              diag_level, status);
+    err = nmp::launch_sflx<double, false>(e->dparams, a, stream);
+  }
+  return err == hipSuccess ? NMP_OK : NMP_E_DEVICE;
+}
+
+}  // namespace
+
+extern "C" {
+
+int nmp_abi_version(void) { return NMP_ABI_VERSION; }
+
+const char* nmp_strerror(int code) {
+  switch (code) {
+    case NMP_OK: return "ok";
+    case NMP_E_ARG: return "invalid argument";
+    case NMP_E_TABLE: return "parameter table missing or unreadable";
+    case NMP_E_OPTION: return "physics option out of range";
+    case NMP_E_DEVICE: return "HIP device error";
+    case NMP_E_PRECISION: return "precision must be 4 or 8";
+    default: return "unknown error";
+  }
+}
+
+int nmp_init(const nmp_params* params, const nmp_options* opts, int device, int precision,
+             nmp_engine** out) {
+  if (!params || !opts || !out) return NMP_E_ARG;
+  *out = nullptr;
+  if (precision != 4 && precision != 8) return NMP_E_PRECISION;
+  if (!options_ok(*opts)) return NMP_E_OPTION;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) return NMP_E_DEVICE;
+  if (ensure_device(device) != NMP_OK) return NMP_E_DEVICE;
+  nmp::DevParams host;
+  std::memset(&host, 0, sizeof(host));
+  nmp::pack_dev_params(*params, host);
+  nmp::DevParams* d = nullptr;
+  if (hipMalloc(&d, sizeof(nmp::DevParams)) != hipSuccess) return NMP_E_DEVICE;
+  if (hipMemcpy(d, &host, sizeof(host), hipMemcpyHostToDevice) != hipSuccess) {
+    hipFree(d);
+    return NMP_E_DEVICE;
+  }
+  nmp_engine* e = new (std::nothrow) nmp_engine;
+  if (!e) {
+    hipFree(d);
+    return NMP_E_ARG;
+  }
+  e->device = device;
+  e->precision = precision;
+  const char* m = std::getenv("NMP_MATH");
+  e->math = (m && std::strcmp(m, "fast") == 0) ? 1 : 0;
+  e->opts = *opts;
+  e->dparams = d;
+  *out = e;
+  return NMP_OK;
+}
+
+int nmp_set_math(nmp_engine* eng, int mode) {
+  if (!eng || mode < 0 || mode > 1) return NMP_E_ARG;
+  eng->math = mode;
+  return NMP_OK;
+}
+
+int nmp_engine_info(const nmp_engine* eng, int* device, int* precision, nmp_options* opts) {
+  if (!eng) return NMP_E_ARG;
+  if (device) *device = eng->device;
+  if (precision) *precision = eng->precision;
+  if (opts) *opts = eng->opts;
+  return NMP_OK;
+}
+
+int nmp_step(nmp_engine* eng, int64_t ncol, int64_t ld, const float zsoil[4], float dt,
+             float julian, int32_t yearlen, void* state, int32_t* isnow, const void* static_f,
+             const int32_t* static_i, const void* forcing, void* diag, int diag_level,
+             int32_t* col_status, void* stream) {
+  if (!eng || !zsoil || ncol < 0 || ld < ncol || !state || !isnow || !static_f || !static_i ||
+      !forcing || !col_status)
+    return NMP_E_ARG;
+  if (diag_level < NMP_DIAG_NONE || diag_level > NMP_DIAG_FULL) return NMP_E_ARG;
+  if (diag_level != NMP_DIAG_NONE && !diag) return NMP_E_ARG;
+  if (!(dt > 0.0f) || yearlen <= 0) return NMP_E_ARG;
+  if (ensure_device(eng->device) != NMP_OK) return NMP_E_DEVICE;
+  return launch(eng, ncol, ld, zsoil, dt, julian, yearlen, state, isnow, static_f, static_i,
+                forcing, diag, diag_level, col_status, static_cast<hipStream_t>(stream));
+}
+
+int nmp_run(nmp_engine* eng, int64_t ncol, int64_t ld, const float zsoil[4], float dt,
+            float julian0, int32_t yearlen, int32_t nsteps, void* state, int32_t* isnow,
+            const void* static_f, const int32_t* static_i, const void* forcing,
+            int64_t forcing_stride, int32_t forcing_period, void* diag, int diag_level,
+            int32_t* col_status, void* stream) {
+  if (!eng || nsteps < 0 || forcing_stride < 0 || forcing_period < 0) return NMP_E_ARG;
+  const size_t esz = eng->precision == 4 ? 4 : 8;
+  for (int32_t s = 0; s < nsteps; ++s) {
+    const int32_t fs = forcing_period > 0 ? s % forcing_period : s;
+    const char* f = static_cast<const char*>(forcing) + (size_t)fs * forcing_stride * esz;
+    const float jul = julian0 + (float)s * dt / 86400.0f;
+    const int lvl = (s == nsteps - 1) ? diag_level : NMP_DIAG_NONE;
+    int rc = nmp_step(eng, ncol, ld, zsoil, dt, jul, yearlen, state, isnow, static_f, static_i, f,
+                      diag, lvl, col_status, stream);
+    if (rc != NMP_OK) return rc;
+  }
+  return NMP_OK;
+}
+
+int nmp_state_from_aos(const void* records, int64_t n, int64_t ld, float* state, int32_t* isnow,
+                       int32_t* static_i) {
+  // noahmp_state_t: 42 x 4-byte sequence record (core/module_noahmp_type.f90:10-42)
+  if (!records || n < 0 || ld < n || !state || !isnow) return NMP_E_ARG;
+  const unsigned char* base = static_cast<const unsigned char*>(records);
+  for (int64_t c = 0; c < n; ++c) {
+    float w[42];
+    std::memcpy(w, base + c * 168, 168);
+    int32_t lutyp, sltyp;
+    std::memcpy(&lutyp, base + c * 168 + 11 * 4, 4);
+    std::memcpy(&sltyp, base + c * 168 + 12 * 4, 4);
+    const float* zsoil = &w[3];
+    const float* zsnow = &w[7];  // snow-layer-top heights, +up
+    const int nsnow = (int)std::lround(w[10]);
+    const int isn = -nsnow;
+    isnow[c] = isn;
+    if (static_i) {
+      static_i[NMP_I_VEGTYP * ld + c] = lutyp;
+      static_i[NMP_I_SOILTYP * ld + c] = sltyp;
+    }
+    auto S = [&](int f) -> float& { return state[(int64_t)f * ld + c]; };
+    S(NMP_S_LAI) = w[13];
+    S(NMP_S_SAI) = w[14];
+    S(NMP_S_TV) = w[16];
+    S(NMP_S_CANLIQ) = w[17];
+    S(NMP_S_CANICE) = w[18];
+    float snowh = 0.0f;
+    for (int j = 0; j < 3; ++j) {
+      const bool act = (j - 2) >= isn + 1;
+      S(NMP_S_STC + j) = act ? w[19 + j] : 0.0f;    // snowtmp
+      S(NMP_S_SNLIQ + j) = act ? w[22 + j] : 0.0f;  // snowwat (mass per area in sflx)
+      S(NMP_S_SNICE + j) = act ? w[25 + j] : 0.0f;  // snowice
+    }
+    // snow layer bottoms from the snow surface: top of layer j is zsnow(j) (+up)
+    float top = 0.0f;
+    for (int j = 0; j < 3; ++j)
+      if ((j - 2) >= isn + 1) top = std::fmax(top, zsnow[j]);
+    for (int j = 0; j < 3; ++j) {
+      const bool act = (j - 2) >= isn + 1;
+      const float bottom = (j < 2 && (j + 1 - 2) >= isn + 1) ? zsnow[j + 1] : 0.0f;
+      S(NMP_S_ZSNSO + j) = act ? bottom - top : 0.0f;
+    }
+    if (isn < 0) snowh = top;
+    for (int k = 0; k < 4; ++k) {
+      S(NMP_S_STC + 3 + k) = w[28 + k];                  // soiltmp
+      S(NMP_S_SH2O + k) = w[32 + k];                     // soilwat
+      S(NMP_S_SMC + k) = w[32 + k] + w[36 + k];          // soilwat + soilice
+      S(NMP_S_ZSNSO + 3 + k) = zsoil[k] - snowh;         // layer bottoms from snow surface
+    }
+    S(NMP_S_WA) = w[40];                 // grndwat
+    S(NMP_S_ZWT) = -w[41];               // +up -> positive depth
+    if (isn < 0) S(NMP_S_SNOWH) = snowh;
+  }
+  return NMP_OK;
+}
+
+void nmp_finalize(nmp_engine* eng) {
+  if (!eng) return;
+  if (eng->dparams) {
+    ensure_device(eng->device);
+    hipFree(eng->dparams);
+  }
+  delete eng;
+}
+
+}  // extern "C"

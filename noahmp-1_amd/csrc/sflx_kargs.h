@@ -1,0 +1,35 @@
+// Kernel argument block shared by the launch site (engine.hip) and the
+// kernel (sflx_kernel.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "dev_params.h"
+
+namespace nmp {
+
+struct Opt {
+  int veg, crs, btr, run, sfc, frz, inf, rad, alb, snf, tbot, stc;
+};
+
+template <class T>
+struct KArgs {
+  int64_t ncol, ld;
+  float zsoil[4];
+  float dt, julian;
+  int yearlen;
+  int diag_level;
+  Opt o;
+  T* state;
+  int32_t* isnow;
+  const T* static_f;
+  const int32_t* static_i;
+  const T* forcing;
+  T* diag;
+  int32_t* status;
+};
+
+template <class T, bool R>
+hipError_t launch_sflx(const DevParams* dparams, const KArgs<T>& a, hipStream_t stream);
+
+}  // namespace nmp

@@ -1,0 +1,2508 @@
+// Noah-MP column time step (noahmp_sflx) as one HIP kernel for gfx950.
+//
+// One lane owns one land column for the whole step: atm -> phenology ->
+// energy (radiation, canopy/ground Newton iterations, snow/soil heat
+// diffusion, phase change) -> water (canopy, snow layers, Richards,
+// groundwater) -> carbon -> balance checks.  Reference:
+// /root/reference/core/module_noahmp_func.f90 (line numbers in comments).
+//
+// MI355X mapping
+//  - SoA field-major state in HBM: each of the 56 state fields, 12 forcing
+//    fields and 12 static fields is one coalesced 256 B (fp32) wave load.
+//  - Lookup tables (DevParams, ~9 KB) staged once per workgroup into LDS;
+//    per-lane type lookups are ds_reads.
+//  - Snow/soil layer arrays (7 layers) live in VGPRs: every layer loop is fully
+//    unrolled over the 7 (or 3 / 4) static slots and predicated on the
+//    column's active range, and the few truly dynamic subscripts (top layer
+//    ISNOW+1, water-table layer) go through select chains (dget/dset), so no
+//    array is ever demoted to scratch.
+//  - Data-dependent Newton / bisection loops diverge per lane under the exec
+//    mask; wave-uniform option branches become scalar branches.
+#include <hip/hip_runtime.h>
+
+#include "dev_params.h"
+#include "sflx_kargs.h"
+#include "sflx_math.h"
+
+namespace nmp {
+
+template <class T>
+struct Col {
+  // static
+  int lutyp, sltyp, slptyp, isc, ist, ice;
+  T lat, zref, shdfac, shdmax, tbot, foln;
+  // forcing
+  T sfctmp, sfcprs, psfc, uu, vv, q2, soldn, lwdn, prcp, cosz, co2air, o2air;
+  // prognostic state
+  T stc[7], zsnso[7], snice[3], snliq[3], sh2o[4], smc[4];
+  T tv, tg, tah, eah, fwet, canliq, canice, qsfc, snowh, sneqv, sneqvo, albold, tauss, qsnow;
+  T zwt, wa, wt, wslake, lai, sai, lfmass, rtmass, stmass, wood, stblcp, fastcp, cm, ch;
+  int isnow;
+  // per-step layer work arrays
+  T dz[7], ficeold[3], sice[4], btrani[4], df[7], hcpct[7], fact[7];
+  int imelt[7];
+  int status;
+};
+
+// physical constants: core/module_noahmp_const.f90:14-35
+#define MPE L(1.0E-6)
+#define GRAV L(9.80616)
+#define SB L(5.67E-8)
+#define RGAS L(8.3144598)
+#define KARMAN L(0.40)
+#define TFRZ L(273.15)
+#define HSUB L(2.8440E6)
+#define HVAP L(2.5104E6)
+#define HFUS L(0.3336E6)
+#define CWAT L(4.188E6)
+#define CICE L(2.094E6)
+#define CPAIR L(1004.64)
+#define TKWAT L(0.6)
+#define TKICE L(2.2)
+#define RAIR L(287.04)
+#define RVAP L(461.269)
+#define DENWAT L(1000.0)
+#define DENICE L(917.0)
+
+#define DEV __device__ __forceinline__
+
+// ---------------------------------------------------------------------------
+// esat: func.f90:3692-3736
+template <class T>
+DEV void esat(T t, T& esw, T& esi, T& desw, T& desi) {
+  esw = L(100.) * (L(6.107799961) + t * (L(4.436518521E-01) + t * (L(1.428945805E-02) +
+        t * (L(2.650648471E-04) + t * (L(3.031240396E-06) + t * (L(2.034080948E-08) +
+        t * L(6.136820929E-11)))))));
+  esi = L(100.) * (L(6.109177956) + t * (L(5.034698970E-01) + t * (L(1.886013408E-02) +
+        t * (L(4.176223716E-04) + t * (L(5.824720280E-06) + t * (L(4.838803174E-08) +
+        t * L(1.838826904E-10)))))));
+  desw = L(100.) * (L(4.438099984E-01) + t * (L(2.857002636E-02) + t * (L(7.938054040E-04) +
+         t * (L(1.215215065E-05) + t * (L(1.036561403E-07) + t * (L(3.532421810e-10) +
+         t * L(-7.090244804E-13)))))));
+  desi = L(100.) * (L(5.030305237E-01) + t * (L(3.773255020E-02) + t * (L(1.267995369E-03) +
+         t * (L(2.477563108E-05) + t * (L(3.005693132E-07) + t * (L(2.158542548E-09) +
+         t * L(7.131097725E-12)))))));
+}
+
+template <class T>
+DEV T tdc(T t) { return rmin(L(50.0), rmax(L(-50.0), (t - TFRZ))); }
+
+// tdfcnd: func.f90:1500-1595
+template <class T, bool R>
+DEV T tdfcnd(const SoilRec& S, T smc, T sh2o) {
+  typedef Mth<T, R> M;
+  T smcmax = (T)S.smcmax, quartz = (T)S.quartz;
+  T satratio = smc / smcmax;
+  T thkw = L(0.57);
+  T thkqtz = L(7.7);
+  T thks = M::pow(thkqtz, quartz) * M::exp2(L(1.0) - quartz);  // 2.0**x -> exp2
+  T xunfroz = sh2o / smc;
+  T xu = xunfroz * smcmax;
+  T thksat = M::pow(thks, L(1.0) - smcmax) * M::pow(TKICE, smcmax - xu) * M::pow(thkw, xu);
+  T gammd = (L(1.0) - smcmax) * L(2700.0);
+  T thkdry = (L(0.135) * gammd + L(64.7)) / (L(2700.0) - L(0.947) * gammd);
+  T ake;
+  if ((sh2o + L(0.0005)) < smc)
+    ake = satratio;
+  else
+    ake = (satratio > L(0.1)) ? M::log10(satratio) + L(1.0) : L(0.0);
+  return ake * (thksat - thkdry) + thkdry;
+}
+
+// twostream: func.f90:2215-2462 for one band / beam type
+template <class T, bool R>
+DEV void twostream(const DevParams& P, const VegRec& V, const Opt& o, int ib, int ic, T cosz,
+                   T vai, T fwet, T t, const T (&albgrd)[2], const T (&albgri)[2],
+                   const T (&rho)[2], const T (&tau)[2], T fveg, T& fab, T& fre, T& ftd, T& fti,
+                   T& gdir, T& bgap, T& wgap) {
+  typedef Mth<T, R> M;
+  const T PAI = L(3.14159265);
+  T gap = L(0.0), kopen = L(0.0);
+  if (vai == L(0.0)) {
+    gap = L(1.0);
+    kopen = L(1.0);
+  } else {
+    if (o.rad == 1) {
+      T rc = (T)V.rcrown;
+      T denfveg = -M::log(rmax(L(1.0) - fveg, L(0.01))) / (PAI * p2(rc));
+      T hd = (T)V.hvt - (T)V.hvb;
+      T bb = L(0.5) * hd;
+      T thetap = M::atan(bb / rc * M::tan(M::acos(rmax(L(0.01), cosz))));
+      bgap = M::exp(-denfveg * PAI * p2(rc) / M::cos(thetap));
+      T fa = vai / (L(1.33) * PAI * p3(rc) * (bb / rc) * denfveg);
+      T newvai = hd * fa;
+      wgap = (L(1.0) - bgap) * M::exp(-L(0.5) * newvai / cosz);
+      gap = rmin(L(1.0) - fveg, bgap + wgap);
+      kopen = L(0.05);
+    }
+    if (o.rad == 2) {
+      gap = L(0.0);
+      kopen = L(0.0);
+    }
+    if (o.rad == 3) {
+      gap = L(1.0) - fveg;
+      kopen = L(1.0) - fveg;
+    }
+  }
+  T coszi = rmax(L(0.001), cosz);
+  T chil = rmin(rmax((T)V.xl, L(-0.4)), L(0.6));
+  if (fabs(chil) <= L(0.01)) chil = L(0.01);
+  T phi1 = L(0.5) - L(0.633) * chil - L(0.330) * chil * chil;
+  T phi2 = L(0.877) * (L(1.) - L(2.) * phi1);
+  gdir = phi1 + phi2 * coszi;
+  T ext = gdir / coszi;
+  T avmu = (L(1.) - phi1 / phi2 * M::log((phi1 + phi2) / phi1)) / phi2;
+  T omegal = rho[ib] + tau[ib];
+  T tmp0 = gdir + phi2 * coszi;
+  T tmp1 = phi1 * coszi;
+  T asu = L(0.5) * omegal * gdir / tmp0 * (L(1.) - tmp1 / tmp0 * M::log((tmp1 + tmp0) / tmp1));
+  T betadl = (L(1.) + avmu * ext) / (omegal * avmu * ext) * asu;
+  T betail = L(0.5) * (rho[ib] + tau[ib] + (rho[ib] - tau[ib]) * p2((L(1.) + chil) / L(2.))) /
+             omegal;
+  T tmp2;
+  if (t > TFRZ) {
+    tmp0 = omegal;
+    tmp1 = betadl;
+    tmp2 = betail;
+  } else {
+    T oms = (T)P.g.omegas[ib];
+    tmp0 = (L(1.0) - fwet) * omegal + fwet * oms;
+    tmp1 = ((L(1.0) - fwet) * omegal * betadl + fwet * oms * (T)P.g.betads) / tmp0;
+    tmp2 = ((L(1.0) - fwet) * omegal * betail + fwet * oms * (T)P.g.betais) / tmp0;
+  }
+  T omega = tmp0, betad = tmp1, betai = tmp2;
+  T b = L(1.) - omega + omega * betai;
+  T c = omega * betai;
+  tmp0 = avmu * ext;
+  T d = tmp0 * omega * betad;
+  T f = tmp0 * omega * (L(1.) - betad);
+  tmp1 = b * b - c * c;
+  T h = M::sqrt(tmp1) / avmu;
+  T sigma = tmp0 * tmp0 - tmp1;
+  if (fabs(sigma) < L(1.e-6)) sigma = copysign(L(1.e-6), sigma);
+  T p1 = b + avmu * h;
+  T pp2 = b - avmu * h;
+  T pp3 = b + tmp0;
+  T pp4 = b - tmp0;
+  T s1 = M::exp(-h * vai);
+  T s2 = M::exp(-ext * vai);
+  T alb = (ic == 0) ? albgrd[ib] : albgri[ib];
+  T u1 = b - c / alb;
+  T u2 = b - c * alb;
+  T u3 = f + c * alb;
+  tmp2 = u1 - avmu * h;
+  T tmp3 = u1 + avmu * h;
+  T d1 = p1 * tmp2 / s1 - pp2 * tmp3 * s1;
+  T tmp4 = u2 + avmu * h;
+  T tmp5 = u2 - avmu * h;
+  T d2 = tmp4 / s1 - tmp5 * s1;
+  T h1 = -d * pp4 - c * f;
+  T tmp6 = d - h1 * pp3 / sigma;
+  T tmp7 = (d - c - h1 / sigma * (u1 + tmp0)) * s2;
+  T h2 = (tmp6 * tmp2 / s1 - pp2 * tmp7) / d1;
+  T h3 = -(tmp6 * tmp3 * s1 - p1 * tmp7) / d1;
+  T h4 = -f * pp3 - c * d;
+  T tmp8 = h4 / sigma;
+  T tmp9 = (u3 - tmp8 * (u2 - tmp0)) * s2;
+  T h5 = -(tmp8 * tmp4 / s1 + tmp9) / d2;
+  T h6 = (tmp8 * tmp5 * s1 + tmp9) / d2;
+  T h7 = (c * tmp2) / (d1 * s1);
+  T h8 = (-c * tmp3 * s1) / d1;
+  T h9 = tmp4 / (d2 * s1);
+  T h10 = (-tmp5 * s1) / d2;
+  if (ic == 0) {
+    ftd = s2 * (L(1.0) - gap) + gap;
+    fti = (h4 * s2 / sigma + h5 * s1 + h6 / s1) * (L(1.0) - gap);
+    fre = (h1 / sigma + h2 + h3) * (L(1.0) - gap) + albgrd[ib] * gap;
+  } else {
+    ftd = L(0.);
+    fti = (h9 * s1 + h10 / s1) * (L(1.0) - kopen) + kopen;
+    fre = (h7 + h8) * (L(1.0) - kopen) + albgri[ib] * kopen;
+  }
+  fab = L(1.0) - fre - (L(1.0) - albgrd[ib]) * ftd - (L(1.0) - albgri[ib]) * fti;
+}
+
+// sfcdif1: func.f90:3353-3508
+template <class T, bool R>
+DEV void sfcdif1(int iter, T sfctmp, T rhoair, T h, T qair, T zlvl, T zpd, T z0m, T z0h, T ur,
+                 T mpe, T& moz, int& mozsgn, T& fm, T& fh, T& fm2, T& fh2, T& cm, T& ch, T& fv,
+                 int& status) {
+  typedef Mth<T, R> M;
+  T mozold = moz;
+  if (zlvl <= zpd) status |= NMP_ST_ZLVL;
+  T tmpcm = M::log((zlvl - zpd) / z0m);
+  T tmpch = M::log((zlvl - zpd) / z0h);
+  T tmpcm2 = M::log((L(2.0) + z0m) / z0m);
+  T tmpch2 = M::log((L(2.0) + z0h) / z0h);
+  T moz2;
+  if (iter == 1) {
+    fv = L(0.0);
+    moz = L(0.0);
+    moz2 = L(0.0);
+  } else {
+    T tvir = (L(1.0) + L(0.61) * qair) * sfctmp;
+    T tmp1 = KARMAN * (GRAV / tvir) * h / (rhoair * CPAIR);
+    if (fabs(tmp1) <= mpe) tmp1 = mpe;
+    T mol = L(-1.0) * p3(fv) / tmp1;
+    moz = rmin((zlvl - zpd) / mol, L(1.0));
+    moz2 = rmin((L(2.0) + z0h) / mol, L(1.0));
+  }
+  if (mozold * moz < L(0.0)) mozsgn = mozsgn + 1;
+  if (mozsgn >= 2) {
+    moz = L(0.0);
+    fm = L(0.0);
+    fh = L(0.0);
+    moz2 = L(0.0);
+    fm2 = L(0.0);
+    fh2 = L(0.0);
+  }
+  T fmnew, fhnew, fm2new, fh2new;
+  if (moz < L(0.0)) {
+    T tmp1 = M::pow(L(1.0) - L(16.0) * moz, L(0.25));
+    T tmp2 = M::log((L(1.0) + tmp1 * tmp1) / L(2.0));
+    T tmp3 = M::log((L(1.0) + tmp1) / L(2.0));
+    fmnew = L(2.0) * tmp3 + tmp2 - L(2.0) * M::atan(tmp1) + L(1.5707963);
+    fhnew = L(2.0) * tmp2;
+    T tmp12 = M::pow(L(1.0) - L(16.0) * moz2, L(0.25));
+    T tmp22 = M::log((L(1.0) + tmp12 * tmp12) / L(2.0));
+    T tmp32 = M::log((L(1.0) + tmp12) / L(2.0));
+    fm2new = L(2.0) * tmp32 + tmp22 - L(2.0) * M::atan(tmp12) + L(1.5707963);
+    fh2new = L(2.0) * tmp22;
+  } else {
+    fmnew = L(-5.0) * moz;
+    fhnew = fmnew;
+    fm2new = L(-5.0) * moz2;
+    fh2new = fm2new;
+  }
+  if (iter == 1) {
+    fm = fmnew;
+    fh = fhnew;
+    fm2 = fm2new;
+    fh2 = fh2new;
+  } else {
+    fm = L(0.5) * (fm + fmnew);
+    fh = L(0.5) * (fh + fhnew);
+    fm2 = L(0.5) * (fm2 + fm2new);
+    fh2 = L(0.5) * (fh2 + fh2new);
+  }
+  fh = rmin(fh, L(0.9) * tmpch);
+  fm = rmin(fm, L(0.9) * tmpcm);
+  fh2 = rmin(fh2, L(0.9) * tmpch2);
+  fm2 = rmin(fm2, L(0.9) * tmpcm2);
+  T cmfm = tmpcm - fm;
+  T chfh = tmpch - fh;
+  T cm2fm2 = tmpcm2 - fm2;
+  T ch2fh2 = tmpch2 - fh2;
+  if (fabs(cmfm) <= mpe) cmfm = mpe;
+  if (fabs(chfh) <= mpe) chfh = mpe;
+  if (fabs(cm2fm2) <= mpe) cm2fm2 = mpe;
+  if (fabs(ch2fh2) <= mpe) ch2fh2 = mpe;
+  cm = KARMAN * KARMAN / (cmfm * cmfm);
+  ch = KARMAN * KARMAN / (cmfm * chfh);
+  fv = ur * M::sqrt(cm);
+}
+
+// sfcdif2 (Chen97, opt_sfc=2): func.f90:3511-3689
+template <class T, bool R>
+DEV void sfcdif2(int iter, T z0, T thz0, T thlm, T sfcspd, T czil, T zlm, T& akms, T& akhs,
+                 T& rlmo, T& wstar2, T& ustar) {
+  typedef Mth<T, R> M;
+  const T WWST = L(1.2);
+  const T WWST2 = WWST * WWST;
+  const T VKRM = L(0.40), EXCM = L(0.001);
+  const T BETA = L(1.0) / L(270.0);
+  const T BTG = BETA * GRAV;
+  const T ELFC = VKRM * BTG;
+  const T WOLD = L(0.15);
+  const T WNEW = L(1.0) - WOLD;
+  const T PIHF = L(3.14159265) / L(2.);
+  T zilfc = -czil * VKRM * L(258.2);
+  T zu = z0;
+  T rdz = L(1.0) / zlm;
+  T cxch = EXCM * rdz;
+  T dthv = thlm - thz0;
+  T du2 = rmax(sfcspd * sfcspd, L(1.E-4));
+  T btgh = BTG * L(1000.0);
+  if (iter == 1) {
+    if (btgh * akhs * dthv != L(0.0))
+      wstar2 = WWST2 * M::pow(fabs(btgh * akhs * dthv), L(2.0) / L(3.0));
+    else
+      wstar2 = L(0.0);
+    ustar = rmax(M::sqrt(akms * M::sqrt(du2 + wstar2)), L(0.07));
+    rlmo = ELFC * akhs * dthv / p3(ustar);
+  }
+  T zt = rmax(L(1.0E-6), M::exp(zilfc * M::sqrt(ustar * z0)) * z0);
+  T zslu = zlm + zu;
+  T zslt = zlm + zt;
+  T rlogu = M::log(zslu / zu);
+  T rlogt = M::log(zslt / zt);
+  T zetalt = rmax(zslt * rlmo, L(-5.0));
+  rlmo = zetalt / zslt;
+  T zetalu = zslu * rlmo;
+  T zetau = zu * rlmo;
+  T zetat = zt * rlmo;
+  T simm, simh;
+  if (rlmo < L(0.0)) {
+    T xlu = M::sqrt(M::sqrt(L(1.0) - L(16.0) * zetalu));
+    T xlt = M::sqrt(M::sqrt(L(1.0) - L(16.0) * zetalt));
+    T xu = M::sqrt(M::sqrt(L(1.0) - L(16.0) * zetau));
+    T xt = M::sqrt(M::sqrt(L(1.0) - L(16.0) * zetat));
+    auto pspmu = [&](T xx) {
+      return L(-2.0) * M::log((xx + L(1.0)) * L(0.5)) - M::log((xx * xx + L(1.0)) * L(0.5)) +
+             L(2.0) * M::atan(xx) - PIHF;
+    };
+    auto psphu = [&](T xx) { return L(-2.0) * M::log((xx * xx + L(1.0)) * L(0.5)); };
+    T psmz = pspmu(xu);
+    simm = pspmu(xlu) - psmz + rlogu;
+    T pshz = psphu(xt);
+    simh = psphu(xlt) - pshz + rlogt;
+  } else {
+    zetalu = rmin(zetalu, L(1.0));
+    zetalt = rmin(zetalt, L(1.0));
+    T psmz = L(5.0) * zetau;
+    simm = L(5.0) * zetalu - psmz + rlogu;
+    T pshz = L(5.0) * zetat;
+    simh = L(5.0) * zetalt - pshz + rlogt;
+  }
+  ustar = rmax(M::sqrt(akms * M::sqrt(du2 + wstar2)), L(0.07));
+  zt = rmax(L(1.E-6), M::exp(zilfc * M::sqrt(ustar * z0)) * z0);
+  zslt = zlm + zt;
+  rlogt = M::log(zslt / zt);
+  T ustark = ustar * VKRM;
+  akms = rmax(ustark / simm, cxch);
+  akhs = rmax(ustark / simh, cxch);
+  if (btgh * akhs * dthv != L(0.0))
+    wstar2 = WWST2 * M::pow(fabs(btgh * akhs * dthv), L(2.0) / L(3.0));
+  else
+    wstar2 = L(0.0);
+  T rlmn = ELFC * akhs * dthv / p3(ustar);
+  rlmo = rlmo * WOLD + rlmn * WNEW;
+}
+
+// ragrb: func.f90:3260-3350
+template <class T, bool R>
+DEV void ragrb(const VegRec& V, int iter, T vai, T rhoair, T hg, T tah, T zpd, T z0mg, T z0hg,
+               T hcan, T uc, T z0h, T fv, T cwp, T mpe, T& fhg, T& rahg, T& rb) {
+  typedef Mth<T, R> M;
+  T mozg = L(0.0);
+  if (iter > 1) {
+    T tmp1 = KARMAN * (GRAV / tah) * hg / (rhoair * CPAIR);
+    if (fabs(tmp1) <= mpe) tmp1 = mpe;
+    T molg = L(-1.) * p3(fv) / tmp1;
+    mozg = rmin((zpd - z0mg) / molg, L(1.0));
+  }
+  T fhgnew = (mozg < L(0.0)) ? M::pow(L(1.0) - L(15.0) * mozg, L(-0.25)) : L(1.0) + L(4.7) * mozg;
+  fhg = (iter == 1) ? fhgnew : L(0.5) * (fhg + fhgnew);
+  T cwpc = M::sqrt(cwp * vai * hcan * fhg);
+  T tmp1 = M::exp(-cwpc * z0hg / hcan);
+  T tmp2 = M::exp(-cwpc * (z0h + zpd) / hcan);
+  T tmprah2 = hcan * M::exp(cwpc) / cwpc * (tmp1 - tmp2);
+  T kh = rmax(KARMAN * fv * (hcan - zpd), mpe);
+  rahg = tmprah2 / kh;
+  T tmprb = cwpc * L(50.0) / (L(1.0) - M::exp(-cwpc / L(2.0)));
+  rb = tmprb * M::sqrt((T)V.dleaf / uc);
+}
+
+// stomata (Ball-Berry bisection): func.f90:3739-3887
+template <class T, bool R>
+DEV void stomata(const VegRec& V, T igs, T sfcprs, T sfctmp, T apar, T tv, T ea, T ei, T o2,
+                 T co2, T foln, T btran, T rb, T& rs, T& psn) {
+  typedef Mth<T, R> M;
+  const T CIERR = L(5.0E-2);
+  T cf = sfcprs / (RGAS * sfctmp) * L(1.0e06);
+  rs = L(1.0) / (T)V.bp * cf;
+  psn = L(0.0);
+  if (apar <= L(0.0)) return;
+  T fnf = rmin(foln / rmax(MPE, (T)V.folnmx), L(1.0));
+  T tc = tv - TFRZ;
+  T ppf = L(4.6) * apar;
+  T j = ppf * (T)V.qe25;
+  T ex = (tc - L(25.0)) / L(10.0);
+  T kc = (T)V.kc25 * M::pow((T)V.akc, ex);
+  T ko = (T)V.ko25 * M::pow((T)V.ako, ex);
+  T awc = kc * (L(1.0) + o2 / ko);
+  T cp = L(0.5) * kc / ko * o2 * L(0.21);
+  T vcmx = (T)V.vcmx25 /
+           (L(1.0) + M::exp((L(-2.2E05) + L(710.0) * (tc + TFRZ)) / (L(8.314) * (tc + TFRZ)))) *
+           fnf * btran * (M::pow((T)V.avcmx, ex));
+  T rlb = rb / cf;
+  T cihigh = L(1.5) * co2, cilow = L(0.0);
+  const int c3c4 = V.c3c4;
+  const T mp = (T)V.mp, bp = (T)V.bp;
+#pragma unroll 1
+  for (int iter = 1; iter <= 20; ++iter) {
+    T ci = L(0.5) * (cihigh + cilow);
+    T wc = (T)NAN, wj = (T)NAN, we = (T)NAN;  // SAVEd nan4 init (func.f90:3854-3856)
+    if (c3c4 == 1) {
+      wj = rmax(ci - cp, L(0.0)) * j / (ci + L(2.0) * cp);
+      wc = rmax(ci - cp, L(0.0)) * vcmx / (ci + awc);
+      we = L(0.5) * vcmx;
+    } else if (c3c4 == 2) {
+      wj = j;
+      wc = vcmx;
+      we = L(4000.0) * vcmx * ci / sfcprs;
+    }
+    psn = rmin(rmin(wj, wc), we) * igs;
+    T cs = rmax(co2 - L(1.37) * rlb * sfcprs * psn, MPE);
+    T a = mp * psn * sfcprs * ea / (cs * ei) + bp;
+    T b = (mp * psn * sfcprs / cs + bp) * rlb - L(1.0);
+    T c = -rlb;
+    T q = (b >= L(0.0)) ? L(-0.5) * (b + M::sqrt(b * b - L(4.0) * a * c))
+                        : L(-0.5) * (b - M::sqrt(b * b - L(4.0) * a * c));
+    T r1 = q / a;
+    T r2 = c / q;
+    rs = rmax(r1, r2);
+    T fci = rmax(cs - psn * sfcprs * L(1.65) * rs, L(0.0));
+    if (((cihigh - cilow) <= CIERR) || fabs(fci - ci) <= MPE) break;
+    if (fci > ci)
+      cilow = ci;
+    else
+      cihigh = ci;
+  }
+  rs = rs * cf;
+}
+
+// canres + calhum (Jarvis, opt_crs=2): func.f90:3890-3984
+template <class T, bool R>
+DEV void canres(const VegRec& V, T sfcprs, T tv, T par, T eah, T btran, T& rs, T& psn) {
+  typedef Mth<T, R> M;
+  T q2 = L(0.622) * eah / (sfcprs - L(0.378) * eah);
+  q2 = q2 / (L(1.0) + q2);
+  const T A2 = L(17.67), A3 = L(273.15), A4 = L(29.65), ELWV = L(2.501E6);
+  const T A23M4 = A2 * (A3 - A4), E0 = L(0.611), RV = L(461.0), EPS = L(0.622);
+  T es = E0 * M::exp(ELWV / RV * (L(1.) / A3 - L(1.) / tv));
+  T sfcprsx = sfcprs * L(1.E-3);
+  T q2sat = EPS * es / (sfcprsx - es);
+  q2sat = q2sat * L(1.E3);
+  q2sat = q2sat / L(1.E3);
+  (void)A23M4;
+  T ff = L(2.0) * par / (T)V.rgl;
+  T rcs = (ff + (T)V.rsmin / (T)V.rsmax) / (L(1.0) + ff);
+  rcs = rmin(rmax(rcs, L(0.0001)), L(1.0));
+  T rct = L(1.0) - L(0.0016) * p2((T)V.topt - tv);
+  rct = rmin(rmax(rct, L(0.0001)), L(1.0));
+  T rcq = L(1.0) / (L(1.0) + (T)V.hs * rmax(L(0.0), q2sat - q2));
+  rcq = rmin(rmax(rcq, L(0.01)), L(1.0));
+  rs = (T)V.rsmin / (rcs * rct * rcq * btran);
+  psn = (T)NAN;
+}
+
+// rosr12 Thomas solve on layers kt..NL-1 (func.f90:4240-4288), static slots
+template <class T, int NL>
+DEV void rosr12(T (&p)[NL], const T (&a)[NL], const T (&b)[NL], T (&c)[NL], const T (&d)[NL],
+                T (&delta)[NL], int kt) {
+  c[NL - 1] = L(0.0);
+#pragma unroll
+  for (int k = 0; k < NL; ++k) {
+    if (k == kt) {
+      p[k] = -c[k] / b[k];
+      delta[k] = d[k] / b[k];
+    } else if (k > kt) {
+      const int km = k > 0 ? k - 1 : 0;
+      p[k] = -c[k] * (L(1.0) / (b[k] + a[k] * p[km]));
+      delta[k] = (d[k] - a[k] * delta[km]) * (L(1.0) / (b[k] + a[k] * p[km]));
+    }
+  }
+  p[NL - 1] = delta[NL - 1];
+#pragma unroll
+  for (int k = NL - 2; k >= 0; --k)
+    if (k >= kt) p[k] = p[k] * p[k + 1] + delta[k];
+}
+
+// combo: func.f90:5536-5577
+template <class T>
+DEV void combo(T& dz, T& wliq, T& wice, T& t, T dz2, T wliq2, T wice2, T t2) {
+  T dzc = dz + dz2;
+  T wicec = wice + wice2;
+  T wliqc = wliq + wliq2;
+  T h = (CICE * wice + CWAT * wliq) * (t - TFRZ) + HFUS * wliq;
+  T h2 = (CICE * wice2 + CWAT * wliq2) * (t2 - TFRZ) + HFUS * wliq2;
+  T hc = h + h2;
+  T tc;
+  if (hc < L(0.0))
+    tc = TFRZ + hc / (CICE * wicec + CWAT * wliqc);
+  else if (hc <= HFUS * wliqc)
+    tc = TFRZ;
+  else
+    tc = TFRZ + (hc - HFUS * wliqc) / (CICE * wicec + CWAT * wliqc);
+  dz = dzc;
+  wice = wicec;
+  wliq = wliqc;
+  t = tc;
+}
+
+// combine: func.f90:5236-5413.  Snow slots j=0..2 <-> layers -2..0.
+template <class T>
+DEV void combine(Col<T>& c, T& ponding1, T& ponding2) {
+  const int iso = c.isnow;
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    if (j >= iso + 3 && c.snice[j] <= L(0.1)) {
+      if (j != 2) {
+        const int j1 = j < 2 ? j + 1 : 2;
+        c.snliq[j1] = c.snliq[j1] + c.snliq[j];
+        c.snice[j1] = c.snice[j1] + c.snice[j];
+      } else {
+        if (iso < -1) {
+          c.snliq[1] = c.snliq[1] + c.snliq[2];
+          c.snice[1] = c.snice[1] + c.snice[2];
+        } else {
+          if (c.snice[2] >= L(0.0)) {
+            ponding1 = c.snliq[2];
+            c.sneqv = c.snice[2];
+            c.snowh = c.dz[2];
+          } else {
+            ponding1 = c.snliq[2] + c.snice[2];
+            if (ponding1 < L(0.0)) {
+              c.sice[0] = rmax(L(0.0), c.sice[0] + ponding1 / (c.dz[3] * L(1000.0)));
+              ponding1 = L(0.0);
+            }
+            c.sneqv = L(0.0);
+            c.snowh = L(0.0);
+          }
+          c.snliq[2] = L(0.0);
+          c.snice[2] = L(0.0);
+          c.dz[2] = L(0.0);
+        }
+      }
+      // shift the layers above down by one (J > ISNOW+1 .and. ISNOW < -1)
+      if (j > c.isnow + 3 && c.isnow < -1) {
+#pragma unroll
+        for (int i = 2; i >= 1; --i) {
+          if (i <= j && i >= c.isnow + 5) {
+            c.stc[i] = c.stc[i - 1];
+            c.snliq[i] = c.snliq[i - 1];
+            c.snice[i] = c.snice[i - 1];
+            c.dz[i] = c.dz[i - 1];
+          }
+        }
+      }
+      c.isnow = c.isnow + 1;
+    }
+  }
+  if (c.sice[0] < L(0.0)) {
+    c.sh2o[0] = c.sh2o[0] + c.sice[0];
+    c.sice[0] = L(0.0);
+  }
+  if (c.isnow == 0) return;
+  c.sneqv = L(0.0);
+  c.snowh = L(0.0);
+  T zwice = L(0.0), zwliq = L(0.0);
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    if (j >= c.isnow + 3) {
+      c.sneqv = c.sneqv + c.snice[j] + c.snliq[j];
+      c.snowh = c.snowh + c.dz[j];
+      zwice = zwice + c.snice[j];
+      zwliq = zwliq + c.snliq[j];
+    }
+  }
+  if (c.snowh < L(0.025) && c.isnow < 0) {
+    c.isnow = 0;
+    c.sneqv = zwice;
+    ponding2 = zwliq;
+    if (c.sneqv <= L(0.0)) c.snowh = L(0.0);
+  }
+  if (c.isnow < -1) {
+    const int iso2 = c.isnow;
+    int mssi = 1;
+    bool done = false;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      if (!done && i >= iso2 + 3) {
+        const T dzmin = (mssi == 3) ? L(0.1) : L(0.025);
+        if (c.dz[i] < dzmin) {
+          // neighbour: I==ISNOW+1 -> I+1; I==0 -> I-1; else the thinner pair
+          bool up;  // true: neighbour is i-1 (combine into slot i)
+          if (i == 0)
+            up = false;
+          else if (i == 2)
+            up = true;
+          else
+            up = (i == c.isnow + 3) ? false
+                                    : ((c.dz[i - 1] + c.dz[i]) < (c.dz[i + 1] + c.dz[i]));
+          if (!up) {  // J = i+1, L = i
+            const int jj = i < 2 ? i + 1 : 2;
+            combo(c.dz[jj], c.snliq[jj], c.snice[jj], c.stc[jj], c.dz[i], c.snliq[i], c.snice[i],
+                  c.stc[i]);
+#pragma unroll
+            for (int k = 2; k >= 1; --k) {
+              if (k <= jj - 1 && k >= c.isnow + 5) {
+                c.stc[k] = c.stc[k - 1];
+                c.snice[k] = c.snice[k - 1];
+                c.snliq[k] = c.snliq[k - 1];
+                c.dz[k] = c.dz[k - 1];
+              }
+            }
+          } else {  // J = i, L = i-1
+            const int ll = i > 0 ? i - 1 : 0;
+            combo(c.dz[i], c.snliq[i], c.snice[i], c.stc[i], c.dz[ll], c.snliq[ll], c.snice[ll],
+                  c.stc[ll]);
+#pragma unroll
+            for (int k = 2; k >= 1; --k) {
+              if (k <= i - 1 && k >= c.isnow + 5) {
+                c.stc[k] = c.stc[k - 1];
+                c.snice[k] = c.snice[k - 1];
+                c.snliq[k] = c.snliq[k - 1];
+                c.dz[k] = c.dz[k - 1];
+              }
+            }
+          }
+          c.isnow = c.isnow + 1;
+          if (c.isnow >= -1) done = true;
+        } else {
+          mssi = mssi + 1;
+        }
+      }
+    }
+  }
+}
+
+// divide: func.f90:5416-5533
+template <class T>
+DEV void divide(Col<T>& c) {
+  T dz[4] = {L(0.), L(0.), L(0.), L(0.)}, swice[4] = {L(0.), L(0.), L(0.), L(0.)};
+  T swliq[4] = {L(0.), L(0.), L(0.), L(0.)}, tsno[4] = {L(0.), L(0.), L(0.), L(0.)};
+  const int n = -c.isnow;
+#pragma unroll
+  for (int J = 1; J <= 3; ++J) {
+    if (J <= n) {  // DZ(J) = DZSNSO(J+ISNOW): slot J+ISNOW+2
+      const int s = J + c.isnow + 2;
+      dz[J] = dget(c.dz, s);
+      swice[J] = dget(c.snice, s);
+      swliq[J] = dget(c.snliq, s);
+      tsno[J] = dget(c.stc, s);
+    }
+  }
+  int msno = n;
+  if (msno == 1) {
+    if (dz[1] > L(0.05)) {
+      msno = 2;
+      dz[1] = dz[1] / L(2.0);
+      swice[1] = swice[1] / L(2.0);
+      swliq[1] = swliq[1] / L(2.0);
+      dz[2] = dz[1];
+      swice[2] = swice[1];
+      swliq[2] = swliq[1];
+      tsno[2] = tsno[1];
+    }
+  }
+  if (msno > 1) {
+    if (dz[1] > L(0.05)) {
+      T drr = dz[1] - L(0.05);
+      T propor = drr / dz[1];
+      T zwice = propor * swice[1];
+      T zwliq = propor * swliq[1];
+      propor = L(0.05) / dz[1];
+      swice[1] = propor * swice[1];
+      swliq[1] = propor * swliq[1];
+      dz[1] = L(0.05);
+      combo(dz[2], swliq[2], swice[2], tsno[2], drr, zwliq, zwice, tsno[1]);
+      if (msno <= 2 && dz[2] > L(0.20)) {
+        msno = 3;
+        T dtdz = (tsno[1] - tsno[2]) / ((dz[1] + dz[2]) / L(2.));
+        dz[2] = dz[2] / L(2.0);
+        swice[2] = swice[2] / L(2.0);
+        swliq[2] = swliq[2] / L(2.0);
+        dz[3] = dz[2];
+        swice[3] = swice[2];
+        swliq[3] = swliq[2];
+        tsno[3] = tsno[2] - dtdz * dz[2] / L(2.0);
+        if (tsno[3] >= TFRZ)
+          tsno[3] = tsno[2];
+        else
+          tsno[2] = tsno[2] + dtdz * dz[2] / L(2.0);
+      }
+    }
+  }
+  if (msno > 2) {
+    if (dz[2] > L(0.2)) {
+      T drr = dz[2] - L(0.2);
+      T propor = drr / dz[2];
+      T zwice = propor * swice[2];
+      T zwliq = propor * swliq[2];
+      propor = L(0.2) / dz[2];
+      swice[2] = propor * swice[2];
+      swliq[2] = propor * swliq[2];
+      dz[2] = L(0.2);
+      combo(dz[3], swliq[3], swice[3], tsno[3], drr, zwliq, zwice, tsno[2]);
+    }
+  }
+  c.isnow = -msno;
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    if (j >= c.isnow + 3) {  // DZSNSO(J) = DZ(J-ISNOW): local index j-isnow-2
+      const int s = j - c.isnow - 2;
+      c.dz[j] = dget(dz, s);
+      c.snice[j] = dget(swice, s);
+      c.snliq[j] = dget(swliq, s);
+      c.stc[j] = dget(tsno, s);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// noahmp_sflx for one column: func.f90:66-476
+template <class T, bool R>
+DEV void sflx_column(const DevParams& P, const KArgs<T>& A, Col<T>& c, T (&dout)[NMP_NDIAG_FULL],
+                     T& t2m_out) {
+  typedef Mth<T, R> M;
+  const Opt& o = A.o;
+  const VegRec& V = P.veg[c.lutyp - 1];
+  const SoilRec& S = P.soil[c.sltyp - 1];
+  const T DT = (T)A.dt;
+  const T zsoil[4] = {(T)A.zsoil[0], (T)A.zsoil[1], (T)A.zsoil[2], (T)A.zsoil[3]};
+  const T smcmax = (T)S.smcmax, smcwlt = (T)S.smcwlt, smcref = (T)S.smcref;
+  const T bexp = (T)S.bexp, psisat = (T)S.psisat;
+  const int nroot = V.nroot;
+
+  // FICEOLD from the state at step start (offline-driver convention)
+#pragma unroll
+  for (int j = 0; j < 3; ++j)
+    c.ficeold[j] = (j >= c.isnow + 3) ? c.snice[j] / (c.snice[j] + c.snliq[j]) : L(0.0);
+
+  // atm: func.f90:479-531
+  T pair = c.sfcprs;
+  T thair = c.sfctmp * M::pow(c.sfcprs / pair, RAIR / CPAIR);
+  T qair = c.q2;
+  T eair = qair * c.sfcprs / (L(0.622) + L(0.378) * qair);
+  T rhoair = (c.sfcprs - L(0.378) * eair) / (RAIR * c.sfctmp);
+  T qprecc = L(0.10) * c.prcp;
+  T qprecl = L(0.90) * c.prcp;
+  T swdown = (c.cosz <= L(0.0)) ? L(0.0) : c.soldn;
+  T solad = swdown * L(0.7) * L(0.5);
+  T solai = swdown * L(0.3) * L(0.5);
+
+  // layer thickness (:322-328)
+#pragma unroll
+  for (int k = 0; k < 7; ++k) {
+    const int km = k > 0 ? k - 1 : 0;
+    if (k == c.isnow + 3)
+      c.dz[k] = -c.zsnso[k];
+    else if (k > c.isnow + 3)
+      c.dz[k] = c.zsnso[km] - c.zsnso[k];
+    else
+      c.dz[k] = L(0.0);
+  }
+  // root-zone temperature (:332-335)
+  T troot = L(0.0);
+  {
+    const T zr = -(nroot > 0 ? (T)zget(A.zsoil, nroot - 1) : L(1.0));
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (k < nroot) troot = troot + c.stc[k + 3] * c.dz[k + 3] / zr;
+  }
+
+  // phenology: func.f90:534-630
+  if (o.veg == 1 || o.veg == 3 || o.veg == 4) {
+    T yl = (T)A.yearlen;
+    T jul = (T)A.julian;
+    T day = (c.lat >= L(0.0)) ? jul : fmod(jul + (L(0.5) * yl), yl);
+    T t = L(12.0) * day / yl;
+    int it1 = (int)(t + L(0.5));
+    int it2 = it1 + 1;
+    T wt1 = ((T)it1 + L(0.5)) - t;
+    T wt2 = L(1.0) - wt1;
+    if (it1 < 1) it1 = 12;
+    if (it2 > 12) it2 = 1;
+    c.lai = wt1 * (T)V.lai12m[it1 - 1] + wt2 * (T)V.lai12m[it2 - 1];
+    c.sai = wt1 * (T)V.sai12m[it1 - 1] + wt2 * (T)V.sai12m[it2 - 1];
+  }
+  if (c.sai < L(0.05)) c.sai = L(0.0);
+  if (c.lai < L(0.05) || c.sai == L(0.0)) c.lai = L(0.0);
+  if (c.lutyp == P.g.iswater || c.lutyp == P.g.isbarren || c.lutyp == P.g.isice ||
+      c.lutyp == P.g.isurban) {
+    c.lai = L(0.0);
+    c.sai = L(0.0);
+  }
+  T elai, esai, igs, htop;
+  {
+    T hvt = (T)V.hvt, hvb = (T)V.hvb;
+    T db = rmin(rmax(c.snowh - hvb, L(0.0)), hvt - hvb);
+    T fb = db / rmax(L(1.0E-06), hvt - hvb);
+    if (hvt > L(0.0) && hvt <= L(1.0)) {
+      T snowhc = hvt * M::exp(-c.snowh / L(0.2));
+      fb = rmin(c.snowh, snowhc) / snowhc;
+    }
+    elai = c.lai * (L(1.0) - fb);
+    esai = c.sai * (L(1.0) - fb);
+    if (esai < L(0.05)) esai = L(0.0);
+    if (elai < L(0.05) || esai == L(0.0)) elai = L(0.0);
+    igs = (c.tv > (T)V.tmin) ? L(1.0) : L(0.0);
+    htop = hvt;
+  }
+  // vegetation fraction (:366-380)
+  T fveg = L(0.0);
+  if (o.veg == 1) {
+    fveg = c.shdfac;
+    if (fveg <= L(0.01)) fveg = L(0.01);
+  } else if (o.veg == 2 || o.veg == 3) {
+    fveg = L(1.0) - M::exp(L(-0.52) * (c.lai + c.sai));
+    if (fveg <= L(0.01)) fveg = L(0.01);
+  } else if (o.veg == 4 || o.veg == 5) {
+    fveg = c.shdmax;
+    if (fveg <= L(0.01)) fveg = L(0.01);
+  } else {
+    c.status |= NMP_ST_OPTVEG;
+  }
+  if (c.lutyp == P.g.isurban || c.lutyp == P.g.isbarren) fveg = L(0.0);
+  if (elai + esai == L(0.0)) fveg = L(0.0);
+
+  // ===================== energy: func.f90:735-1338 =====================
+  const T Z0 = L(0.01);
+  const int kt = c.isnow + 3;  // top active layer slot
+  T irc = 0, shc = 0, irg = 0, shg = 0, evg = 0, evc = 0, tr = 0, ghv = 0, psnsun = 0, psnsha = 0;
+  T t2mv = 0, q2v = 0, chv = 0, chleaf = 0, chuc = 0, chv2 = 0, rssun = 0, rssha = 0;
+  T bgap = 0, wgap = 0;
+  T ur = rmax(M::sqrt(c.uu * c.uu + c.vv * c.vv), L(1.0));
+  T vai = elai + esai;
+  const bool veg = vai > L(0.0);
+  T fsno = L(0.0);
+  if (c.snowh > L(0.0)) {
+    T bdsno = c.sneqv / c.snowh;
+    T fmelt = M::pow(bdsno / L(100.0), (T)P.g.mltfct);
+    fsno = M::tanh(c.snowh / (L(2.5) * Z0 * fmelt));
+  }
+  T z0mg;
+  if (c.ist == 2)
+    z0mg = (c.tg <= TFRZ) ? L(0.01) * (L(1.0) - fsno) + fsno * (T)P.g.z0sno : L(0.01);
+  else
+    z0mg = Z0 * (L(1.0) - fsno) + fsno * (T)P.g.z0sno;
+  T zpdg = c.snowh, z0m, zpd;
+  if (veg) {
+    z0m = (T)V.z0mvt;
+    zpd = L(0.65) * htop;
+    if (c.snowh > zpd) zpd = c.snowh;
+  } else {
+    z0m = z0mg;
+    zpd = zpdg;
+  }
+  T zlvl = rmax(zpd, htop) + c.zref;
+  if (zpdg >= zlvl) zlvl = zpdg + c.zref;
+  const T cwp = (T)V.cwpvt;
+
+  // thermoprop + csnow + tdfcnd: func.f90:1341-1595
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    if (j >= kt) {
+      T snicev = rmin(L(1.0), c.snice[j] / (c.dz[j] * DENICE));
+      T epore = L(1.0) - snicev;
+      T snliqv = rmin(epore, c.snliq[j] / (c.dz[j] * DENWAT));
+      T bdsnoi = (c.snice[j] + c.snliq[j]) / c.dz[j];
+      c.hcpct[j] = CICE * snicev + CWAT * snliqv;
+      c.df[j] = L(3.2217E-6) * p2(bdsnoi);
+    } else {
+      c.hcpct[j] = L(0.0);
+      c.df[j] = L(0.0);
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    T sice = c.smc[k] - c.sh2o[k];
+    c.hcpct[k + 3] = c.sh2o[k] * CWAT + (L(1.0) - smcmax) * (T)P.g.csoil +
+                     (smcmax - c.smc[k]) * CPAIR + sice * CICE;
+    c.df[k + 3] = tdfcnd<T, R>(S, c.smc[k], c.sh2o[k]);
+  }
+  if (c.lutyp == P.g.isurban) {
+#pragma unroll
+    for (int k = 3; k < 7; ++k) c.df[k] = L(3.24);
+  }
+  if (c.ist == 2) {
+#pragma unroll
+    for (int k = 3; k < 7; ++k) {
+      const bool warm = c.stc[k] > TFRZ;
+      c.hcpct[k] = warm ? CWAT : CICE;
+      c.df[k] = warm ? TKWAT : TKICE;
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 7; ++k) c.fact[k] = (k >= kt) ? DT / (c.hcpct[k] * c.dz[k]) : L(0.0);
+  if (c.isnow == 0)
+    c.df[3] = (c.df[3] * c.dz[3] + L(0.35) * c.snowh) / (c.snowh + c.dz[3]);
+  else
+    c.df[3] = (c.df[3] * c.dz[3] + c.df[2] * c.dz[2]) / (c.dz[2] + c.dz[3]);
+
+  // radiation: albedo + twostream + surrad (func.f90:1598-2005)
+  T albgrd[2] = {L(0.), L(0.)}, albgri[2] = {L(0.), L(0.)}, albd[2] = {L(0.), L(0.)};
+  T albi[2] = {L(0.), L(0.)}, fabd[2] = {L(0.), L(0.)}, fabi[2] = {L(0.), L(0.)};
+  T ftdd[2] = {L(0.), L(0.)}, ftid[2] = {L(0.), L(0.)}, ftii[2] = {L(0.), L(0.)};
+  T fsun = L(0.0);
+  if (c.cosz > L(0.0)) {
+    const T mpe6 = L(1.0E-06);
+    T rho[2], tau[2];
+    T vaia = elai + esai;
+#pragma unroll
+    for (int ib = 0; ib < 2; ++ib) {
+      T wl = elai / rmax(vaia, mpe6);
+      T ws = esai / rmax(vaia, mpe6);
+      rho[ib] = rmax((T)V.rhol[ib] * wl + (T)V.rhos[ib] * ws, mpe6);
+      tau[ib] = rmax((T)V.taul[ib] * wl + (T)V.taus[ib] * ws, mpe6);
+    }
+    // snowage: func.f90:2008-2054
+    T fage;
+    if (c.sneqv <= L(0.0)) {
+      c.tauss = L(0.0);
+    } else if (c.sneqv > L(800.0)) {
+      c.tauss = L(0.0);
+    } else {
+      T dela0 = L(1.0E-6) * DT;
+      T arg = L(5.0E3) * (L(1.0) / TFRZ - L(1.0) / c.tg);
+      T age1 = M::exp(arg);
+      T age2 = M::exp(rmin(L(0.0), L(10.0) * arg));
+      T tage = age1 + age2 + L(0.3);
+      T dela = dela0 * tage;
+      T dels = rmax(L(0.0), c.sneqv - c.sneqvo) / (T)P.g.swemax;
+      T sge = (c.tauss + dela) * (L(1.0) - dels);
+      c.tauss = rmax(L(0.0), sge);
+    }
+    fage = c.tauss / (c.tauss + L(1.0));
+    T albsnd[2] = {L(0.), L(0.)}, albsni[2] = {L(0.), L(0.)};
+    if (o.alb == 1) {  // snowalb_bats: func.f90:2057-2102
+      T sl = L(2.0);
+      T sl1 = L(1.0) / sl;
+      T sl2 = L(2.0) * sl;
+      T cf1 = ((L(1.0) + sl1) / (L(1.0) + sl2 * c.cosz) - sl1);
+      T fzen = rmax(cf1, L(0.0));
+      albsni[0] = L(0.95) * (L(1.0) - L(0.2) * fage);
+      albsni[1] = L(0.65) * (L(1.0) - L(0.5) * fage);
+      albsnd[0] = albsni[0] + L(0.4) * fzen * (L(1.0) - albsni[0]);
+      albsnd[1] = albsni[1] + L(0.4) * fzen * (L(1.0) - albsni[1]);
+    }
+    if (o.alb == 2) {  // snowalb_class: func.f90:2105-2151
+      T alb = L(0.55) + (c.albold - L(0.55)) * M::exp(-L(0.01) * DT / L(3600.0));
+      if (c.qsnow > L(0.0))
+        alb = alb + rmin(c.qsnow * DT, (T)P.g.swemax) * (L(0.84) - alb) / (T)P.g.swemax;
+      albsnd[0] = albsnd[1] = albsni[0] = albsni[1] = alb;
+      c.albold = alb;
+    }
+    // groundalb: func.f90:2154-2212
+#pragma unroll
+    for (int ib = 0; ib < 2; ++ib) {
+      T inc = rmax(L(0.11) - L(0.40) * c.smc[0], L(0.0));
+      T albsod, albsoi;
+      if (c.ist == 1) {
+        albsod = rmin((T)P.g.albsat[c.isc - 1][ib] + inc, (T)P.g.albdry[c.isc - 1][ib]);
+        albsoi = albsod;
+      } else if (c.tg > TFRZ) {
+        albsod = L(0.06) / (M::pow(rmax(L(0.01), c.cosz), L(1.7)) + L(0.15));
+        albsoi = L(0.06);
+      } else {
+        albsod = (T)P.g.alblake[ib];
+        albsoi = albsod;
+      }
+      if (c.ist == 1 && c.isc == 9) {
+        albsod = albsod + L(0.10);
+        albsoi = albsoi + L(0.10);
+      }
+      albgrd[ib] = albsod * (L(1.0) - fsno) + albsnd[ib] * fsno;
+      albgri[ib] = albsoi * (L(1.0) - fsno) + albsni[ib] * fsno;
+    }
+    T gdir = L(0.0);
+#pragma unroll
+    for (int ib = 0; ib < 2; ++ib) {
+      twostream<T, R>(P, V, o, ib, 0, c.cosz, vaia, c.fwet, c.tv, albgrd, albgri, rho, tau, fveg,
+                      fabd[ib], albd[ib], ftdd[ib], ftid[ib], gdir, bgap, wgap);
+      T ftdi_unused;
+      twostream<T, R>(P, V, o, ib, 1, c.cosz, vaia, c.fwet, c.tv, albgrd, albgri, rho, tau, fveg,
+                      fabi[ib], albi[ib], ftdi_unused, ftii[ib], gdir, bgap, wgap);
+    }
+    T ext = gdir / c.cosz * M::sqrt(L(1.0) - rho[0] - tau[0]);
+    fsun = (L(1.0) - M::exp(-ext * vaia)) / rmax(ext * vaia, mpe6);
+    ext = fsun;
+    fsun = (ext < L(0.01)) ? L(0.) : ext;
+  }
+  T fsha = L(1.0) - fsun;
+  T laisun = elai * fsun;
+  T laisha = elai * fsha;
+  T sav, sag, fsa, fsr, parsun, parsha;
+  {
+    T cad0 = solad * fabd[0], cai0 = solai * fabi[0];
+    T cad1 = solad * fabd[1], cai1 = solai * fabi[1];
+    sag = L(0.0);
+    sav = L(0.0);
+    fsa = L(0.0);
+    sav = sav + cad0 + cai0;
+    fsa = fsa + cad0 + cai0;
+    T abs0 = (solad * ftdd[0]) * (L(1.0) - albgrd[0]) +
+             (solad * ftid[0] + solai * ftii[0]) * (L(1.0) - albgri[0]);
+    sag = sag + abs0;
+    fsa = fsa + abs0;
+    sav = sav + cad1 + cai1;
+    fsa = fsa + cad1 + cai1;
+    T abs1 = (solad * ftdd[1]) * (L(1.0) - albgrd[1]) +
+             (solad * ftid[1] + solai * ftii[1]) * (L(1.0) - albgri[1]);
+    sag = sag + abs1;
+    fsa = fsa + abs1;
+    T laifra = elai / rmax(vai, L(1.0E-6));
+    if (fsun > L(0.0)) {
+      parsun = (cad0 + fsun * cai0) * laifra / rmax(laisun, L(1.0E-6));
+      parsha = (fsha * cai0) * laifra / rmax(laisha, L(1.0E-6));
+    } else {
+      parsun = L(0.0);
+      parsha = (cad0 + cai0) * laifra / rmax(laisha, L(1.0E-6));
+    }
+    fsr = (albd[0] * solad + albi[0] * solai) + (albd[1] * solad + albi[1] * solai);
+  }
+  T emv = L(1.0) - M::exp(-(elai + esai) / L(1.0));
+  T emg;
+  if (c.ice == 1)
+    emg = L(0.98) * (L(1.0) - fsno) + L(1.0) * fsno;
+  else if (c.ist == 1)
+    emg = (T)P.g.emssoil * (L(1.0) - fsno) + L(1.0) * fsno;
+  else
+    emg = (T)P.g.emslake * (L(1.0) - fsno) + L(1.0) * fsno;
+  // soil moisture stress (:1117-1140)
+  T btran = L(0.0);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) c.btrani[k] = L(0.0);
+  if (c.ist == 1) {
+    const T zr = -(nroot > 0 ? (T)zget(A.zsoil, nroot - 1) : L(1.0));
+    const T PSIWLT = L(-150.);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      if (k < nroot) {
+        T gx = L(0.0);
+        if (o.btr == 1) gx = (c.sh2o[k] - smcwlt) / (smcref - (smcwlt));
+        if (o.btr == 2 || o.btr == 3) {
+          T psi = rmax(PSIWLT, -psisat * M::pow(rmax(L(0.01), c.sh2o[k]) / smcmax, -bexp));
+          if (o.btr == 2)
+            gx = (L(1.0) - psi / PSIWLT) / (L(1.0) + psisat / PSIWLT);
+          else
+            gx = L(1.0) - M::exp(L(-5.8) * (M::log(PSIWLT / psi)));
+        }
+        gx = rmin(L(1.0), rmax(L(0.0), gx));
+        c.btrani[k] = rmax(MPE, c.dz[k + 3] / zr * gx);
+        btran = btran + c.btrani[k];
+      }
+    }
+    btran = rmax(MPE, btran);
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (k < nroot) c.btrani[k] = c.btrani[k] / btran;
+  }
+  // ground surface resistance (:1143-1169)
+  T rsurf, rhsur;
+  if (c.ist == 2) {
+    rsurf = L(1.0);
+    rhsur = L(1.0);
+  } else {
+    T l_rsurf = (-zsoil[0]) * (M::exp(p5(L(1.0) - rmin(L(1.0), c.sh2o[0] / smcmax))) - L(1.0)) /
+                (L(2.71828) - L(1.0));
+    T d_rsurf = L(2.2E-5) * smcmax * smcmax *
+                M::pow(L(1.0) - smcwlt / smcmax, L(2.0) + L(3.0) / bexp);
+    rsurf = l_rsurf / d_rsurf;
+    if (c.sh2o[0] < L(0.01) && c.snowh == L(0.0)) rsurf = L(1.0E6);
+    T psi = -psisat * M::pow(rmax(L(0.01), c.sh2o[0]) / smcmax, -bexp);
+    rhsur = fsno + (L(1.0) - fsno) * M::exp(psi * GRAV / (RVAP * c.tg));
+  }
+  if (c.lutyp == P.g.isurban && c.snowh == L(0.0)) rsurf = L(1.0E6);
+  const bool frozen_canopy = !(c.tv > TFRZ);
+  const T latheav = frozen_canopy ? HSUB : HVAP;
+  const T gammav = CPAIR * c.sfcprs / (L(0.622) * latheav);
+  const bool frozen_ground = !(c.tg > TFRZ);
+  const T latheag = frozen_ground ? HSUB : HVAP;
+  const T gammag = CPAIR * c.sfcprs / (L(0.622) * latheag);
+  const T stc_top = dget(c.stc, kt), df_top = dget(c.df, kt), dz_top = dget(c.dz, kt);
+
+  // ---- vege_flux: func.f90:2465-2964 ----
+  T tgv = L(0.0), cmv = L(0.0);
+  if (veg && fveg > L(0.0)) {
+    tgv = c.tg;
+    cmv = c.cm;
+    chv = c.ch;
+    const T mpe = L(1E-6);
+    int liter = 0;
+    T fv = L(0.1), h = L(0.0), hg = L(0.0);
+    int mozsgn = 0;
+    T moz = L(0.0), fm = L(0.0), fh = L(0.0), fm2 = L(0.0), fh2 = L(0.0);
+    T fhg = L(0.0), wstar = L(0.0), rahg = L(0.0), rb = L(0.0), cah = L(0.0), cvh = L(0.0);
+    T z0h = z0m;
+    T vaie = rmin(L(6.0), vai / fveg);
+    T laisune = rmin(L(6.0), laisun / fveg);
+    T laishae = rmin(L(6.0), laisha / fveg);
+    T esatw, esati, dsatw, dsati;
+    T tt = tdc(tgv);
+    esat(tt, esatw, esati, dsatw, dsati);
+    T estg = (tt > L(0.0)) ? esatw : esati;
+    c.qsfc = L(0.622) * eair / (c.psfc - L(0.378) * eair);
+    T hcan = htop;
+    T uc = ur * M::log(hcan / z0m) / M::log(zlvl / z0m);
+    if ((hcan - zpd) <= L(0.0)) c.status |= NMP_ST_HCAN;
+    T air = -emv * (L(1.0) + (L(1.0) - emv) * (L(1.0) - emg)) * c.lwdn -
+            emv * emg * SB * p4(tgv);
+    T cir = (L(2.0) - emv * (L(1.0) - emg)) * emv * SB;
+    T rahc = L(1.0);
+#pragma unroll 1
+    for (int iter = 1; iter <= 20; ++iter) {
+      if (o.sfc == 1)
+        sfcdif1<T, R>(iter, c.sfctmp, rhoair, h, qair, zlvl, zpd, z0m, z0h, ur, mpe, moz, mozsgn,
+                      fm, fh, fm2, fh2, cmv, chv, fv, c.status);
+      if (o.sfc == 2) {
+        sfcdif2<T, R>(iter, z0m, c.tah, thair, ur, (T)P.g.czil, zlvl, cmv, chv, moz, wstar, fv);
+        chv = chv / ur;
+        cmv = cmv / ur;
+      }
+      rahc = rmax(L(1.0), L(1.0) / (chv * ur));
+      T rawc = rahc;
+      ragrb<T, R>(V, iter, vaie, rhoair, hg, c.tah, zpd, z0mg, z0mg, hcan, uc, z0h, fv, cwp, mpe,
+                  fhg, rahg, rb);
+      T rawg = rahg;
+      tt = tdc(c.tv);
+      esat(tt, esatw, esati, dsatw, dsati);
+      T estv = (tt > L(0.0)) ? esatw : esati;
+      T destv = (tt > L(0.0)) ? dsatw : dsati;
+      if (iter == 1) {
+        if (o.crs == 1) {
+          stomata<T, R>(V, igs, c.sfcprs, c.sfctmp, parsun, c.tv, c.eah, estv, c.o2air, c.co2air,
+                        c.foln, btran, rb, rssun, psnsun);
+          stomata<T, R>(V, igs, c.sfcprs, c.sfctmp, parsha, c.tv, c.eah, estv, c.o2air, c.co2air,
+                        c.foln, btran, rb, rssha, psnsha);
+        }
+        if (o.crs == 2) {
+          canres<T, R>(V, c.sfcprs, c.tv, parsun, c.eah, btran, rssun, psnsun);
+          canres<T, R>(V, c.sfcprs, c.tv, parsha, c.eah, btran, rssha, psnsha);
+        }
+      }
+      cah = L(1.0) / rahc;
+      cvh = L(2.0) * vaie / rb;
+      T cgh = L(1.0) / rahg;
+      T cond = cah + cvh + cgh;
+      T ata = (c.sfctmp * cah + tgv * cgh) / cond;
+      T bta = cvh / cond;
+      T csh = (L(1.0) - bta) * rhoair * CPAIR * cvh;
+      T caw = L(1.0) / rawc;
+      T cew = c.fwet * vaie / rb;
+      T ctw = (L(1.0) - c.fwet) * (laisune / (rb + rssun) + laishae / (rb + rssha));
+      T cgw = L(1.0) / (rawg + rsurf);
+      cond = caw + cew + ctw + cgw;
+      T aea = (eair * caw + estg * cgw) / cond;
+      T bea = (cew + ctw) / cond;
+      T cev = (L(1.0) - bea) * cew * rhoair * CPAIR / gammav;
+      T ctr = (L(1.0) - bea) * ctw * rhoair * CPAIR / gammav;
+      c.tah = ata + bta * c.tv;
+      c.eah = aea + bea * estv;
+      irc = fveg * (air + cir * p4(c.tv));
+      shc = fveg * rhoair * CPAIR * cvh * (c.tv - c.tah);
+      evc = fveg * rhoair * CPAIR * cew * (estv - c.eah) / gammav;
+      tr = fveg * rhoair * CPAIR * ctw * (estv - c.eah) / gammav;
+      if (c.tv > TFRZ)
+        evc = rmin(c.canliq * latheav / DT, evc);
+      else
+        evc = rmin(c.canice * latheav / DT, evc);
+      T b = sav - irc - shc - evc - tr;
+      T a = fveg * (L(4.0) * cir * p3(c.tv) + csh + (cev + ctr) * destv);
+      T dtv = b / a;
+      irc = irc + fveg * L(4.0) * cir * p3(c.tv) * dtv;
+      shc = shc + fveg * csh * dtv;
+      evc = evc + fveg * cev * destv * dtv;
+      tr = tr + fveg * ctr * destv * dtv;
+      c.tv = c.tv + dtv;
+      h = rhoair * CPAIR * (c.tah - c.sfctmp) / rahc;
+      hg = rhoair * CPAIR * (tgv - c.tah) / rahg;
+      c.qsfc = (L(0.622) * c.eah) / (c.sfcprs - L(0.378) * c.eah);
+      if (liter == 1) break;
+      if (iter >= 5 && fabs(dtv) <= L(0.01) && liter == 0) liter = 1;
+    }
+    // under-canopy fluxes and TG (loop2, :2881-2914)
+    air = -emg * (L(1.0) - emv) * c.lwdn - emg * emv * SB * p4(c.tv);
+    cir = emg * SB;
+    T csh = rhoair * CPAIR / rahg;
+    T cev = rhoair * CPAIR / (gammag * (rahg + rsurf));
+    T cgh = L(2.0) * df_top / dz_top;
+#pragma unroll 1
+    for (int iter = 1; iter <= 5; ++iter) {
+      tt = tdc(tgv);
+      esat(tt, esatw, esati, dsatw, dsati);
+      estg = (tt > L(0.0)) ? esatw : esati;
+      T destg = (tt > L(0.0)) ? dsatw : dsati;
+      irg = cir * p4(tgv) + air;
+      shg = csh * (tgv - c.tah);
+      evg = cev * (estg * rhsur - c.eah);
+      ghv = cgh * (tgv - stc_top);
+      T b = sag - irg - shg - evg - ghv;
+      T a = L(4.0) * cir * p3(tgv) + csh + cev * destg + cgh;
+      T dtg = b / a;
+      irg = irg + L(4.0) * cir * p3(tgv) * dtg;
+      shg = shg + csh * dtg;
+      evg = evg + cev * destg * dtg;
+      ghv = ghv + cgh * dtg;
+      tgv = tgv + dtg;
+    }
+    if (o.stc == 1 && c.snowh > L(0.05) && tgv > TFRZ) {
+      tgv = TFRZ;
+      irg = cir * p4(tgv) - emg * (L(1.0) - emv) * c.lwdn - emg * emv * SB * p4(c.tv);
+      shg = csh * (tgv - c.tah);
+      evg = cev * (estg * rhsur - c.eah);
+      ghv = sag - (irg + shg + evg);
+    }
+    if (o.sfc == 1 || o.sfc == 2) {
+      chv2 = fv * KARMAN / (M::log((L(2.0) + z0h) / z0h) - fh2);
+      if (chv2 < L(1.E-5)) {
+        t2mv = c.tah;
+        q2v = c.qsfc;
+      } else {
+        t2mv = c.tah - (shg + shc / fveg) / (rhoair * CPAIR) * L(1.0) / chv2;
+        q2v = c.qsfc - ((evc + tr) / fveg + evg) / (latheav * rhoair) * L(1.0) / chv2;
+      }
+    }
+    chv = cah;
+    chleaf = cvh;
+    chuc = L(1.0) / rahg;
+  }
+
+  // ---- bare_flux: func.f90:2967-3257 ----
+  T tgb = c.tg, cmb = c.cm, chb = c.ch;
+  T irb, shb, evb, ghb, t2mb = L(0.0), q2b = L(0.0), chb2 = L(0.0);
+  {
+    const T mpe = L(1.0E-6);
+    int mozsgn = 0;
+    T h = L(0.0), fv = L(0.1), moz = L(0.0), fm = L(0.0), fh = L(0.0), fm2 = L(0.0), fh2 = L(0.0);
+    T wstar = L(0.0);
+    T cir = emg * SB;
+    T cgh = L(2.0) * df_top / dz_top;
+    T z0h = z0mg, ehb = L(0.0), csh = L(0.0), cev = L(0.0), estg = L(0.0);
+    T esatw, esati, dsatw, dsati;
+    irb = shb = evb = ghb = L(0.0);
+#pragma unroll 1
+    for (int iter = 1; iter <= 5; ++iter) {
+      if (o.sfc == 1)
+        sfcdif1<T, R>(iter, c.sfctmp, rhoair, h, qair, zlvl, zpdg, z0mg, z0h, ur, mpe, moz,
+                      mozsgn, fm, fh, fm2, fh2, cmb, chb, fv, c.status);
+      if (o.sfc == 2) {
+        sfcdif2<T, R>(iter, z0mg, tgb, thair, ur, (T)P.g.czil, zlvl, cmb, chb, moz, wstar, fv);
+        chb = chb / ur;
+        cmb = cmb / ur;
+        if (c.snowh > L(0.0)) {
+          cmb = rmin(L(0.01), cmb);
+          chb = rmin(L(0.01), chb);
+        }
+      }
+      T rahb = rmax(L(1.0), L(1.0) / (chb * ur));
+      T rawb = rahb;
+      ehb = L(1.0) / rahb;
+      T tt = tdc(tgb);
+      esat(tt, esatw, esati, dsatw, dsati);
+      estg = (tt > L(0.0)) ? esatw : esati;
+      T destg = (tt > L(0.0)) ? dsatw : dsati;
+      csh = rhoair * CPAIR / rahb;
+      cev = rhoair * CPAIR / gammag / (rsurf + rawb);
+      irb = cir * p4(tgb) - emg * c.lwdn;
+      shb = csh * (tgb - c.sfctmp);
+      evb = cev * (estg * rhsur - eair);
+      ghb = cgh * (tgb - stc_top);
+      T b = sag - irb - shb - evb - ghb;
+      T a = L(4.0) * cir * p3(tgb) + csh + cev * destg + cgh;
+      T dtg = b / a;
+      irb = irb + L(4.0) * cir * p3(tgb) * dtg;
+      shb = shb + csh * dtg;
+      evb = evb + cev * destg * dtg;
+      ghb = ghb + cgh * dtg;
+      tgb = tgb + dtg;
+      h = csh * (tgb - c.sfctmp);
+      tt = tdc(tgb);
+      esat(tt, esatw, esati, dsatw, dsati);
+      estg = (tt > L(0.0)) ? esatw : esati;
+      c.qsfc = L(0.622) * (estg * rhsur) / (c.psfc - L(0.378) * (estg * rhsur));
+    }
+    if (o.stc == 1 && c.snowh > L(0.05) && tgb > TFRZ) {
+      tgb = TFRZ;
+      irb = cir * p4(tgb) - emg * c.lwdn;
+      shb = csh * (tgb - c.sfctmp);
+      evb = cev * (estg * rhsur - eair);
+      ghb = sag - (irb + shb + evb);
+    }
+    if (o.sfc == 1 || o.sfc == 2) {
+      chb2 = fv * KARMAN / (M::log((L(2.0) + z0h) / z0h) - fh2);
+      if (chb2 < L(1.0E-5)) {
+        t2mb = tgb;
+        q2b = c.qsfc;
+      } else {
+        t2mb = tgb - shb / (rhoair * CPAIR) * L(1.0) / chb2;
+        q2b = c.qsfc - evb / (latheag * rhoair) * (L(1.0) / chb2 + rsurf);
+      }
+      if (c.lutyp == P.g.isurban) q2b = c.qsfc;
+    }
+    chb = ehb;
+  }
+
+  // tile aggregation (:1246-1282)
+  T fira, fsh, fgev, ssoil, fcev, fctr, t2m;
+  if (veg && fveg > L(0.0)) {
+    fira = fveg * irg + (L(1.0) - fveg) * irb + irc;
+    fsh = fveg * shg + (L(1.0) - fveg) * shb + shc;
+    fgev = fveg * evg + (L(1.0) - fveg) * evb;
+    ssoil = fveg * ghv + (L(1.0) - fveg) * ghb;
+    fcev = evc;
+    fctr = tr;
+    c.tg = fveg * tgv + (L(1.0) - fveg) * tgb;
+    t2m = fveg * t2mv + (L(1.0) - fveg) * t2mb;
+    c.cm = fveg * cmv + (L(1.0) - fveg) * cmb;
+    c.ch = fveg * chv + (L(1.0) - fveg) * chb;
+  } else {
+    fira = irb;
+    fsh = shb;
+    fgev = evb;
+    ssoil = ghb;
+    c.tg = tgb;
+    t2m = t2mb;
+    fcev = L(0.);
+    fctr = L(0.);
+    c.cm = cmb;
+    c.ch = chb;
+    rssun = L(0.0);
+    rssha = L(0.0);
+    tgv = tgb;
+    chv = chb;
+  }
+  T fire = c.lwdn + fira;
+  if (fire <= L(0.0)) c.status |= NMP_ST_FIRE;
+  T emissi = fveg * (emg * (L(1.) - emv) + emv + emv * (L(1.) - emv) * (L(1.) - emg)) +
+             (L(1.) - fveg) * emg;
+  T trad = M::pow((fire - (L(1.0) - emissi) * c.lwdn) / (emissi * SB), L(0.25));
+  T apar = parsun * laisun + parsha * laisha;
+  T psn = psnsun * laisun + psnsha * laisha;
+
+  // tsnosoi + hrt + hstep (func.f90:3987-4237), layers kt..6 in VGPRs
+  {
+    T ai[7], bi[7], ci[7], rhs[7], ddz[7], denom[7], dtsdz[7];
+#pragma unroll
+    for (int k = 0; k < 7; ++k) ai[k] = bi[k] = ci[k] = rhs[k] = ddz[k] = denom[k] = dtsdz[k] = L(0.);
+    const T zbotsno = (T)P.g.zbot - c.snowh;
+    T botflx = L(0.0);
+#pragma unroll
+    for (int k = 0; k < 7; ++k) {
+      const int km = k > 0 ? k - 1 : 0, kp = k < 6 ? k + 1 : 6;
+      if (k == kt) {
+        denom[k] = -c.zsnso[k] * c.hcpct[k];
+        T temp1 = -c.zsnso[kp];
+        ddz[k] = L(2.0) / temp1;
+        dtsdz[k] = L(2.0) * (c.stc[k] - c.stc[kp]) / temp1;
+        rhs[k] = c.df[k] * dtsdz[k] - ssoil - L(0.0);  // EFLUX
+      } else if (k > kt && k < 6) {
+        denom[k] = (c.zsnso[km] - c.zsnso[k]) * c.hcpct[k];
+        T temp1 = c.zsnso[km] - c.zsnso[kp];
+        ddz[k] = L(2.0) / temp1;
+        dtsdz[k] = L(2.0) * (c.stc[k] - c.stc[kp]) / temp1;
+        rhs[k] = (c.df[k] * dtsdz[k] - c.df[km] * dtsdz[km]) - L(0.0);
+      } else if (k == 6) {
+        denom[k] = (c.zsnso[km] - c.zsnso[k]) * c.hcpct[k];
+        if (o.tbot == 1) botflx = L(0.);
+        if (o.tbot == 2) {
+          dtsdz[k] = (c.stc[k] - c.tbot) / (L(0.5) * (c.zsnso[km] + c.zsnso[k]) - zbotsno);
+          botflx = -c.df[k] * dtsdz[k];
+        }
+        rhs[k] = (-botflx - c.df[km] * dtsdz[km]) - L(0.0);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 7; ++k) {
+      const int km = k > 0 ? k - 1 : 0;
+      if (k == kt) {
+        ai[k] = L(0.0);
+        ci[k] = -c.df[k] * ddz[k] / denom[k];
+        if (o.stc == 1) bi[k] = -ci[k];
+        if (o.stc == 2) bi[k] = -ci[k] + c.df[k] / (L(0.5) * c.zsnso[k] * c.zsnso[k] * c.hcpct[k]);
+      } else if (k > kt && k < 6) {
+        ai[k] = -c.df[km] * ddz[km] / denom[k];
+        ci[k] = -c.df[k] * ddz[k] / denom[k];
+        bi[k] = -(ai[k] + ci[k]);
+      } else if (k == 6) {
+        ai[k] = -c.df[km] * ddz[km] / denom[k];
+        ci[k] = L(0.0);
+        bi[k] = -(ai[k] + ci[k]);
+      }
+      if (k >= kt) rhs[k] = rhs[k] / (-denom[k]);
+    }
+    T ciin[7], rhsin[7], pp[7], delta[7];
+#pragma unroll
+    for (int k = 0; k < 7; ++k) {
+      if (k >= kt) {
+        rhs[k] = rhs[k] * DT;
+        ai[k] = ai[k] * DT;
+        bi[k] = L(1.) + bi[k] * DT;
+        ci[k] = ci[k] * DT;
+      }
+      rhsin[k] = rhs[k];
+      ciin[k] = ci[k];
+      pp[k] = L(0.);
+      delta[k] = L(0.);
+    }
+    rosr12<T, 7>(pp, ai, bi, ciin, rhsin, delta, kt);
+#pragma unroll
+    for (int k = 0; k < 7; ++k)
+      if (k >= kt) c.stc[k] = c.stc[k] + pp[k];
+  }
+  if (o.stc == 2) {
+    if (c.snowh > L(0.05) && c.tg > TFRZ) {
+      tgv = TFRZ;
+      tgb = TFRZ;
+      c.tg = (veg && fveg > L(0.0)) ? fveg * tgv + (L(1.0) - fveg) * tgb : tgb;
+    }
+  }
+
+  // phasechange: func.f90:4291-4491
+  T qmelt = L(0.0), ponding = L(0.0);
+  {
+    T hm[7], xm[7], wmass0[7], wice0[7], mice[7], mliq[7], supercool[7];
+    T xmf = L(0.0);
+#pragma unroll
+    for (int k = 0; k < 7; ++k) {
+      supercool[k] = L(0.0);
+      if (k < 3) {
+        mice[k] = c.snice[k];
+        mliq[k] = c.snliq[k];
+      } else {
+        mliq[k] = c.sh2o[k - 3] * c.dz[k] * L(1000.0);
+        mice[k] = (c.smc[k - 3] - c.sh2o[k - 3]) * c.dz[k] * L(1000.0);
+      }
+      c.imelt[k] = 0;
+      hm[k] = L(0.0);
+      xm[k] = L(0.0);
+      wice0[k] = mice[k];
+      wmass0[k] = mice[k] + mliq[k];
+    }
+    if (c.ist == 1) {
+#pragma unroll
+      for (int k = 3; k < 7; ++k) {
+        if (o.frz == 1 && c.stc[k] < TFRZ) {
+          T smp = HFUS * (TFRZ - c.stc[k]) / (GRAV * c.stc[k]);
+          supercool[k] = smcmax * M::pow(smp / psisat, L(-1.0) / bexp);
+          supercool[k] = supercool[k] * c.dz[k] * L(1000.0);
+        }
+        if (o.frz == 2) {  // frh2o: func.f90:4494-4598
+          T tkelv = c.stc[k], smc = c.smc[k - 3], sh2o = c.sh2o[k - 3];
+          T free_;
+          T bx = bexp;
+          if (bexp > L(5.5)) bx = L(5.5);
+          if (tkelv > (TFRZ - L(1.0E-3))) {
+            free_ = smc;
+          } else {
+            const T CK = L(8.0);
+            T swl = smc - sh2o;
+            if (swl > (smc - L(0.02))) swl = smc - L(0.02);
+            if (swl < L(0.0)) swl = L(0.0);
+            int nlog = 0, kcount = 0;
+#pragma unroll 1
+            while ((nlog < 10) && (kcount == 0)) {
+              nlog = nlog + 1;
+              T dfv = M::log((psisat * GRAV / HFUS) * p2(L(1.0) + CK * swl) *
+                             M::pow(smcmax / (smc - swl), bx)) -
+                      M::log(-(tkelv - TFRZ) / tkelv);
+              T den = L(2.0) * CK / (L(1.0) + CK * swl) + bx / (smc - swl);
+              T swlk = swl - dfv / den;
+              if (swlk > (smc - L(0.02))) swlk = smc - L(0.02);
+              if (swlk < L(0.0)) swlk = L(0.0);
+              T dswl = fabs(swlk - swl);
+              swl = swlk;
+              if (dswl <= L(0.005)) kcount = kcount + 1;
+            }
+            free_ = smc - swl;
+            if (kcount == 0) {
+              c.status |= NMP_ST_FLERCH;
+              T fk = M::pow((HFUS / (GRAV * (-psisat))) * ((tkelv - TFRZ) / tkelv), L(-1.0) / bx) *
+                     smcmax;
+              if (fk < L(0.02)) fk = L(0.02);
+              free_ = rmin(fk, smc);
+            }
+          }
+          supercool[k] = free_ * c.dz[k] * L(1000.0);
+        }
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 7; ++k) {
+      if (k >= kt) {
+        if (mice[k] > L(0.0) && c.stc[k] >= TFRZ) c.imelt[k] = 1;
+        if (mliq[k] > supercool[k] && c.stc[k] < TFRZ) c.imelt[k] = 2;
+        if (k == 3 && c.isnow == 0 && c.sneqv > L(0.0) && c.stc[k] >= TFRZ) c.imelt[k] = 1;
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 7; ++k) {
+      if (k >= kt) {
+        if (c.imelt[k] > 0) {
+          hm[k] = (c.stc[k] - TFRZ) / c.fact[k];
+          c.stc[k] = TFRZ;
+        }
+        if (c.imelt[k] == 1 && hm[k] < L(0.0)) {
+          hm[k] = L(0.0);
+          c.imelt[k] = 0;
+        }
+        if (c.imelt[k] == 2 && hm[k] > L(0.0)) {
+          hm[k] = L(0.0);
+          c.imelt[k] = 0;
+        }
+        xm[k] = hm[k] * DT / HFUS;
+      }
+    }
+    if (c.isnow == 0 && c.sneqv > L(0.0) && xm[3] > L(0.0)) {
+      T temp1 = c.sneqv;
+      c.sneqv = rmax(L(0.0), temp1 - xm[3]);
+      T propor = c.sneqv / temp1;
+      c.snowh = rmax(L(0.0), propor * c.snowh);
+      T heatr = hm[3] - HFUS * (temp1 - c.sneqv) / DT;
+      if (heatr > L(0.0)) {
+        xm[3] = heatr * DT / HFUS;
+        hm[3] = heatr;
+      } else {
+        xm[3] = L(0.0);
+        hm[3] = L(0.0);
+      }
+      qmelt = rmax(L(0.0), (temp1 - c.sneqv)) / DT;
+      xmf = HFUS * qmelt;
+      ponding = temp1 - c.sneqv;
+    }
+#pragma unroll
+    for (int k = 0; k < 7; ++k) {
+      if (k >= kt && c.imelt[k] > 0 && fabs(hm[k]) > L(0.0)) {
+        T heatr = L(0.0);
+        if (xm[k] > L(0.0)) {
+          mice[k] = rmax(L(0.0), wice0[k] - xm[k]);
+          heatr = hm[k] - HFUS * (wice0[k] - mice[k]) / DT;
+        } else if (xm[k] < L(0.0)) {
+          if (k < 3) {
+            mice[k] = rmin(wmass0[k], wice0[k] - xm[k]);
+          } else {
+            if (wmass0[k] < supercool[k]) {
+              mice[k] = L(0.0);
+            } else {
+              mice[k] = rmin(wmass0[k] - supercool[k], wice0[k] - xm[k]);
+              mice[k] = rmax(mice[k], L(0.0));
+            }
+          }
+          heatr = hm[k] - HFUS * (wice0[k] - mice[k]) / DT;
+        }
+        mliq[k] = rmax(L(0.0), wmass0[k] - mice[k]);
+        if (fabs(heatr) > L(0.0)) {
+          c.stc[k] = c.stc[k] + c.fact[k] * heatr;
+          if (k < 3 && mliq[k] * mice[k] > L(0.0)) c.stc[k] = TFRZ;
+        }
+        xmf = xmf + HFUS * (wice0[k] - mice[k]) / DT;
+        if (k < 3) qmelt = qmelt + rmax(L(0.0), (wice0[k] - mice[k])) / DT;
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      if (k >= kt) {
+        c.snliq[k] = mliq[k];
+        c.snice[k] = mice[k];
+      }
+    }
+#pragma unroll
+    for (int k = 3; k < 7; ++k) {
+      c.sh2o[k - 3] = mliq[k] / (L(1000.0) * c.dz[k]);
+      c.smc[k - 3] = (mliq[k] + mice[k]) / (L(1000.0) * c.dz[k]);
+    }
+    (void)xmf;
+  }
+  // ===================== end energy =====================
+
+#pragma unroll
+  for (int k = 0; k < 4; ++k) c.sice[k] = rmax(L(0.0), c.smc[k] - c.sh2o[k]);
+  c.sneqvo = c.sneqv;
+  const T qvap = rmax(fgev / latheag, L(0.0));
+  const T qdew = fabs(rmin(fgev / latheag, L(0.0)));
+  const T edir = qvap - qdew;
+
+  // ===================== water: func.f90:4601-4804 =====================
+  T ecan, etran, runsrf = L(0.0), runsub = L(0.0), qsnbot = L(0.0), ponding1 = L(0.0);
+  T ponding2 = L(0.0), fpice = L(0.0), snoflow = L(0.0);
+  T qrain, snowhin;
+  {
+    // canwater: func.f90:4807-5046
+    T fp = L(0.0), qintr, qdripr, qthror, qints, qdrips, qthros, qevac, qdewc, qfroc, qsubc;
+    if (o.snf == 1) {
+      if (c.sfctmp > TFRZ + L(2.5))
+        fpice = L(0.0);
+      else if (c.sfctmp <= TFRZ + L(0.5))
+        fpice = L(1.0);
+      else if (c.sfctmp <= TFRZ + L(2.0))
+        fpice = L(1.0) - (L(-54.632) + L(0.2) * c.sfctmp);
+      else
+        fpice = L(0.6);
+    }
+    if (o.snf == 2) fpice = (c.sfctmp >= TFRZ + L(2.2)) ? L(0.) : L(1.0);
+    if (o.snf == 3) fpice = (c.sfctmp >= TFRZ) ? L(0.0) : L(1.0);
+    T bdfall = rmin(L(120.0), L(67.92) + L(51.25) * M::exp((c.sfctmp - TFRZ) / L(2.59)));
+    T rain = (qprecc + qprecl) * (L(1.0) - fpice);
+    T snow = (qprecc + qprecl) * fpice;
+    if (qprecc + qprecl > L(0.0)) fp = (qprecc + qprecl) / (L(10.0) * qprecc + qprecl);
+    T maxliq = (T)V.canwmxp * (elai + esai);
+    if ((elai + esai) > L(0.0)) {
+      qintr = fveg * rain * fp;
+      qintr = rmin(qintr, (maxliq - c.canliq) / DT * (L(1.0) - M::exp(-rain * DT / maxliq)));
+      qintr = rmax(qintr, L(0.0));
+      qdripr = fveg * rain - qintr;
+      qthror = (L(1.0) - fveg) * rain;
+    } else {
+      qintr = L(0.0);
+      qdripr = L(0.0);
+      qthror = rain;
+    }
+    if (!frozen_canopy) {
+      etran = rmax(fctr / HVAP, L(0.0));
+      qevac = rmax(fcev / HVAP, L(0.0));
+      qdewc = fabs(rmin(fcev / HVAP, L(0.0)));
+      qsubc = L(0.0);
+      qfroc = L(0.0);
+    } else {
+      etran = rmax(fctr / HSUB, L(0.0));
+      qevac = L(0.0);
+      qdewc = L(0.0);
+      qsubc = rmax(fcev / HSUB, L(0.0));
+      qfroc = fabs(rmin(fcev / HSUB, L(0.0)));
+    }
+    qevac = rmin(c.canliq / DT, qevac);
+    c.canliq = rmax(L(0.0), c.canliq + (qintr + qdewc - qevac) * DT);
+    if (c.canliq <= L(1.0E-6)) c.canliq = L(0.0);
+    T maxsno = L(6.6) * (L(0.27) + L(46.0) / bdfall) * (elai + esai);
+    if ((elai + esai) > L(0.0)) {
+      qints = fveg * snow * fp;
+      qints = rmin(qints, (maxsno - c.canice) / DT * (L(1.0) - M::exp(-snow * DT / maxsno)));
+      qints = rmax(qints, L(0.0));
+      T ft = rmax(L(0.0), (c.tv - L(270.15)) / L(1.87E5));
+      T fvw = M::sqrt(c.uu * c.uu + c.vv * c.vv) / L(1.56E5);
+      qdrips = rmax(L(0.0), c.canice) * (fvw + ft);
+      qthros = (L(1.0) - fveg) * snow + (fveg * snow - qints);
+    } else {
+      qints = L(0.0);
+      qdrips = L(0.0);
+      qthros = snow;
+    }
+    qsubc = rmin(c.canice / DT, qsubc);
+    c.canice = rmax(L(0.0), c.canice + (qints - qdrips) * DT + (qfroc - qsubc) * DT);
+    if (c.canice <= L(1.0E-6)) c.canice = L(0.0);
+    if (c.canice > L(0.0))
+      c.fwet = rmax(L(0.0), c.canice) / rmax(maxsno, L(1.0E-06));
+    else
+      c.fwet = rmax(L(0.0), c.canliq) / rmax(maxliq, L(1.0E-06));
+    c.fwet = M::pow(rmin(c.fwet, L(1.0)), L(0.667));
+    if (c.canice > L(1.0E-6) && c.tv > TFRZ) {
+      T qmeltc = rmin(c.canice / DT, (c.tv - TFRZ) * CICE * c.canice / DENICE / (DT * HFUS));
+      c.canice = rmax(L(0.0), c.canice - qmeltc * DT);
+      c.canliq = rmax(L(0.0), c.canliq + qmeltc * DT);
+      c.tv = c.fwet * TFRZ + (L(1.0) - c.fwet) * c.tv;
+    }
+    if (c.canliq > L(1.0E-6) && c.tv < TFRZ) {
+      T qfrzc = rmin(c.canliq / DT, (TFRZ - c.tv) * CWAT * c.canliq / DENWAT / (DT * HFUS));
+      c.canliq = rmax(L(0.0), c.canliq - qfrzc * DT);
+      c.canice = rmax(L(0.0), c.canice + qfrzc * DT);
+      c.tv = c.fwet * TFRZ + (L(1.0) - c.fwet) * c.tv;
+    }
+    ecan = qevac + qsubc - qdewc - qfroc;
+    qrain = qdripr + qthror;
+    c.qsnow = qdrips + qthros;
+    snowhin = c.qsnow / bdfall;
+    if (c.ist == 2 && c.tg > TFRZ) {
+      c.qsnow = L(0.0);
+      snowhin = L(0.0);
+    }
+  }
+  T qsnsub = (c.sneqv > L(0.0)) ? rmin(qvap, c.sneqv / DT) : L(0.0);
+  T qseva = qvap - qsnsub;
+  T qsnfro = (c.sneqv > L(0.0)) ? qdew : L(0.0);
+  T qsdew = qdew - qsnfro;
+
+  // snowwater: func.f90:5049-5174.  Two passes share one copy of `combine`:
+  // pass 0 = snowfall + compact + combine, pass 1 = divide + snowh2o head +
+  // its conditional combine.
+#pragma unroll 1
+  for (int pass = 0; pass < 2; ++pass) {
+    bool do_combine;
+    if (pass == 0) {
+      // snowfall: func.f90:5177-5233
+      bool newnode = false;
+      if (c.isnow == 0 && c.qsnow > L(0.0)) {
+        c.snowh = c.snowh + snowhin * DT;
+        c.sneqv = c.sneqv + c.qsnow * DT;
+      }
+      if (c.isnow == 0 && c.qsnow > L(0.0) && c.snowh >= L(0.025)) {
+        c.isnow = -1;
+        newnode = true;
+        c.dz[2] = c.snowh;
+        c.snowh = L(0.0);
+        c.stc[2] = rmin(L(273.16), c.sfctmp);
+        c.snice[2] = c.sneqv;
+        c.snliq[2] = L(0.0);
+      }
+      if (c.isnow < 0 && !newnode && c.qsnow > L(0.0)) {
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+          if (j == c.isnow + 3) {
+            c.snice[j] = c.snice[j] + c.qsnow * DT;
+            c.dz[j] = c.dz[j] + snowhin * DT;
+          }
+        }
+      }
+      // compact: func.f90:5580-5677
+      if (c.isnow < 0) {
+        const T C2 = L(21.e-3), C3 = L(2.5e-6), C4 = L(0.04), C5 = L(2.0), DM = L(100.0);
+        const T ETA0 = L(0.8e+6);
+        T burden = L(0.0);
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+          if (j >= c.isnow + 3) {
+            T wx = c.snice[j] + c.snliq[j];
+            T fice = c.snice[j] / wx;
+            T voidf = L(1.) - (c.snice[j] / DENICE + c.snliq[j] / DENWAT) / c.dz[j];
+            if (voidf > L(0.001) && c.snice[j] > L(0.1)) {
+              T bi = c.snice[j] / c.dz[j];
+              T td = rmax(L(0.0), TFRZ - c.stc[j]);
+              T dexpf = M::exp(-C4 * td);
+              T ddz1 = -C3 * dexpf;
+              if (bi > DM) ddz1 = ddz1 * M::exp(L(-46.0E-3) * (bi - DM));
+              if (c.snliq[j] > L(0.01) * c.dz[j]) ddz1 = ddz1 * C5;
+              T ddz2 = -(burden + L(0.5) * wx) * M::exp(L(-0.08) * td - C2 * bi) / ETA0;
+              T ddz3;
+              if (c.imelt[j] == 1) {
+                ddz3 = rmax(L(0.0), (c.ficeold[j] - fice) / rmax(L(1.E-6), c.ficeold[j]));
+                ddz3 = -ddz3 / DT;
+              } else {
+                ddz3 = L(0.0);
+              }
+              T pdzdtc = (ddz1 + ddz2 + ddz3) * DT;
+              pdzdtc = rmax(L(-0.5), pdzdtc);
+              c.dz[j] = c.dz[j] * (L(1.0) + pdzdtc);
+            }
+            burden = burden + wx;
+          }
+        }
+      }
+      do_combine = c.isnow < 0;
+    } else {
+      if (c.isnow < 0) divide(c);
+      // snowh2o head: func.f90:5726-5766
+      if (c.sneqv == L(0.0)) {
+        c.sice[0] = c.sice[0] + (qsnfro - qsnsub) * DT / (c.dz[3] * L(1000.0));
+        if (c.sice[0] < L(0.0)) {
+          c.sh2o[0] = c.sh2o[0] + c.sice[0];
+          c.sice[0] = L(0.0);
+        }
+      }
+      if (c.isnow == 0 && c.sneqv > L(0.0)) {
+        T temp = c.sneqv;
+        c.sneqv = c.sneqv - qsnsub * DT + qsnfro * DT;
+        T propor = c.sneqv / temp;
+        c.snowh = rmax(L(0.0), propor * c.snowh);
+        if (c.sneqv < L(0.0)) {
+          c.sice[0] = c.sice[0] + c.sneqv / (c.dz[3] * L(1000.0));
+          c.sneqv = L(0.0);
+          c.snowh = L(0.0);
+        }
+        if (c.sice[0] < L(0.0)) {
+          c.sh2o[0] = c.sh2o[0] + c.sice[0];
+          c.sice[0] = L(0.0);
+        }
+      }
+      if (c.snowh <= L(1.0E-8) || c.sneqv <= L(1.0E-6)) {
+        c.snowh = L(0.0);
+        c.sneqv = L(0.0);
+      }
+      do_combine = false;
+      if (c.isnow < 0) {
+        T wgdif = L(0.0);
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+          if (j == c.isnow + 3) {
+            wgdif = c.snice[j] - qsnsub * DT + qsnfro * DT;
+            c.snice[j] = wgdif;
+          }
+        }
+        do_combine = (wgdif < L(1.0E-6) && c.isnow < 0);
+      }
+    }
+    if (do_combine) combine(c, ponding1, ponding2);
+  }
+  // snowh2o tail: func.f90:5773-5818
+  {
+    if (c.isnow < 0) {
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        if (j == c.isnow + 3) {
+          c.snliq[j] = c.snliq[j] + qrain * DT;
+          c.snliq[j] = rmax(L(0.0), c.snliq[j]);
+        }
+      }
+    }
+    T vol_liq[3] = {L(0.), L(0.), L(0.)}, vol_ice[3] = {L(0.), L(0.), L(0.)};
+    T epor[3] = {L(0.), L(0.), L(0.)};
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      if (j >= c.isnow + 3) {
+        vol_ice[j] = rmin(L(1.0), c.snice[j] / (c.dz[j] * DENICE));
+        epor[j] = L(1.0) - vol_ice[j];
+        vol_liq[j] = rmin(epor[j], c.snliq[j] / (c.dz[j] * DENWAT));
+      }
+    }
+    T qin = L(0.0), qout = L(0.0);
+    const T ssi = (T)P.g.ssi;
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      if (j >= c.isnow + 3) {
+        c.snliq[j] = c.snliq[j] + qin;
+        if (j < 2) {
+          const int j1 = j < 2 ? j + 1 : 2;
+          if (epor[j] < L(0.05) || epor[j1] < L(0.05)) {
+            qout = L(0.0);
+          } else {
+            qout = rmax(L(0.0), (vol_liq[j] - ssi * epor[j]) * c.dz[j]);
+            qout = rmin(qout, (L(1.0) - vol_ice[j1] - vol_liq[j1]) * c.dz[j1]);
+          }
+        } else {
+          qout = rmax(L(0.0), (vol_liq[j] - ssi * epor[j]) * c.dz[j]);
+        }
+        qout = qout * L(1000.0);
+        c.snliq[j] = c.snliq[j] - qout;
+        qin = qout;
+      }
+    }
+    qsnbot = qout / DT;
+  }
+  // snowwater tail: empty layers, glacier overflow, layer geometry
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    if (j <= c.isnow + 2) {
+      c.snice[j] = L(0.0);
+      c.snliq[j] = L(0.0);
+      c.stc[j] = L(0.0);
+      c.dz[j] = L(0.0);
+      c.zsnso[j] = L(0.0);
+    }
+  }
+  if (c.sneqv > L(2000.0)) {
+    T bdsnow = c.snice[2] / c.dz[2];
+    snoflow = (c.sneqv - L(2000.0));
+    c.snice[2] = c.snice[2] - snoflow;
+    c.dz[2] = c.dz[2] - snoflow / bdsnow;
+    snoflow = snoflow / DT;
+  }
+  if (c.isnow < 0) {
+    c.sneqv = L(0.0);
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+      if (j >= c.isnow + 3) c.sneqv = c.sneqv + c.snice[j] + c.snliq[j];
+  }
+  {
+    const int kt2 = c.isnow + 3;
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+      if (j >= kt2) c.dz[j] = -c.dz[j];
+    c.dz[3] = zsoil[0];
+#pragma unroll
+    for (int k = 1; k < 4; ++k) c.dz[k + 3] = (zsoil[k] - zsoil[k - 1]);
+#pragma unroll
+    for (int k = 0; k < 7; ++k) {
+      const int km = k > 0 ? k - 1 : 0;
+      if (k == kt2)
+        c.zsnso[k] = c.dz[k];
+      else if (k > kt2)
+        c.zsnso[k] = c.zsnso[km] + c.dz[k];
+    }
+#pragma unroll
+    for (int k = 0; k < 7; ++k)
+      if (k >= kt2) c.dz[k] = -c.dz[k];
+  }
+  // frozen ground (:4744-4752)
+  if (frozen_ground) {
+    c.sice[0] = c.sice[0] + (qsdew - qseva) * DT / (c.dz[3] * L(1000.0));
+    qsdew = L(0.0);
+    qseva = L(0.0);
+    if (c.sice[0] < L(0.0)) {
+      c.sh2o[0] = c.sh2o[0] + c.sice[0];
+      c.sice[0] = L(0.0);
+    }
+  }
+  T qinsrf = (ponding + ponding1 + ponding2) / DT * L(0.001);
+  if (c.isnow == 0)
+    qinsrf = qinsrf + (qsnbot + qsdew + qrain) * L(0.001);
+  else
+    qinsrf = qinsrf + (qsnbot + qsdew) * L(0.001);
+  qseva = qseva * L(0.001);
+  T etrani[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) etrani[k] = (k < nroot) ? etran * c.btrani[k] * L(0.001) : L(0.0);
+
+  if (c.ist == 2) {
+    runsrf = L(0.);
+    if (c.wslake >= L(5000.)) runsrf = qinsrf * L(1000.0);
+    c.wslake = c.wslake + (qinsrf - qseva) * L(1000.0) * DT - runsrf * DT;
+  } else {
+    // soilh2o: func.f90:5822-6048
+    T wcnd[4], fcr[4];
+    T qdrain = L(0.0), fcrmax = L(0.0);
+    T qinfil = L(0.0);
+    T rsat = L(0.0);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      T ep = rmax(L(1.0E-4), (smcmax - c.sice[k]));
+      rsat = rsat + rmax(L(0.0), c.sh2o[k] - ep) * c.dz[k + 3];
+      c.sh2o[k] = rmin(ep, c.sh2o[k]);
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      T fice = rmin(L(1.0), c.sice[k] / smcmax);
+      fcr[k] = rmax(L(0.0), M::exp(-L(4.0) * (L(1.0) - fice)) - M::exp(-L(4.0))) /
+               (L(1.0) - M::exp(-L(4.0)));
+    }
+    T sicemax = L(0.0);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      if (c.sice[k] > sicemax) sicemax = c.sice[k];
+      if (fcr[k] > fcrmax) fcrmax = fcr[k];
+    }
+    if (o.run == 2) {  // zwteq: func.f90:6051-6100
+      T wd1 = L(0.0);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) wd1 = wd1 + (smcmax - c.sh2o[k]) * c.dz[k + 3];
+      T dzfine = L(3.0) * (-zsoil[3]) / (T)100;
+      c.zwt = L(-3.0) * zsoil[3] - L(0.001);
+      T wd2 = L(0.0);
+#pragma unroll 1
+      for (int k = 1; k <= 100; ++k) {
+        T zfine = (T)k * dzfine;
+        T temp = L(1.0) + (c.zwt - zfine) / psisat;
+        wd2 = wd2 + smcmax * (L(1.0) - M::pow(temp, L(-1.0) / bexp)) * dzfine;
+        if (fabs(wd2 - wd1) <= L(0.01)) {
+          c.zwt = zfine;
+          break;
+        }
+      }
+      runsub = (L(1.0) - fcrmax) * L(4.0) * M::exp(-(T)P.g.timean) * M::exp(-L(2.0) * c.zwt);
+    }
+    if (c.lutyp == P.g.isurban) fcr[0] = L(0.95);
+    if (o.run == 1 || o.run == 2) {
+      const T fff = (o.run == 1) ? L(6.0) : L(2.0);
+      T fsat = (o.run == 1) ? (T)P.g.fsatmax * M::exp(L(-0.5) * fff * (c.zwt - L(2.0)))
+                            : (T)P.g.fsatmax * M::exp(L(-0.5) * fff * c.zwt);
+      if (qinsrf > L(0.0)) {
+        runsrf = qinsrf * ((L(1.0) - fcr[0]) * fsat + fcr[0]);
+        qinfil = qinsrf - runsrf;
+      }
+    }
+    if (o.run == 3 && qinsrf > L(0.0)) {  // infil: func.f90:6103-6196
+      T dt1 = DT / L(86400.0);
+      T smcav = smcmax - smcwlt;
+      T dmax1 = -zsoil[0] * smcav;
+      T dice = -zsoil[0] * c.sice[0];
+      dmax1 = dmax1 * (L(1.0) - (c.sh2o[0] + c.sice[0] - smcwlt) / smcav);
+      T dd = dmax1;
+#pragma unroll
+      for (int k = 1; k < 4; ++k) {
+        dice = dice + (zsoil[k - 1] - zsoil[k]) * c.sice[k];
+        T dmaxk = (zsoil[k - 1] - zsoil[k]) * smcav;
+        dmaxk = dmaxk * (L(1.0) - (c.sh2o[k] + c.sice[k] - smcwlt) / smcav);
+        dd = dd + dmaxk;
+      }
+      T val = (L(1.0) - M::exp(-(T)S.kdt * dt1));
+      T ddt = dd * val;
+      T px = rmax(L(0.0), qinsrf * DT);
+      T infmax = (px * (ddt / (px + ddt))) / DT;
+      T fcrl = L(1.0);
+      if (dice > L(1.0E-2)) {
+        T acrt = L(3.0) * (T)S.frzx / dice;
+        T sum = L(1.0);
+        sum = sum + (acrt * acrt) / L(2.0);  // J=1: ACRT**2 / 2!
+        sum = sum + (acrt) / L(1.0);         // J=2: ACRT**1 / 1
+        fcrl = L(1.0) - M::exp(-acrt) * sum;
+      }
+      infmax = infmax * fcrl;
+      T factr = rmax(L(0.01), c.sh2o[0] / smcmax);
+      T wcnd1 = (T)S.dksat * M::pow(factr, L(2.0) * bexp + L(3.0));
+      infmax = rmax(infmax, wcnd1);
+      infmax = rmin(infmax, px);
+      runsrf = rmax(L(0.0), qinsrf - infmax);
+      qinfil = qinsrf - runsrf;
+    }
+    if (o.run == 4) {
+      T smctot = L(0.0), dztot = L(0.0);
+      bool stop = false;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        if (!stop) {
+          dztot = dztot + c.dz[k + 3];
+          smctot = smctot + c.smc[k] * c.dz[k + 3];
+          if (dztot >= L(2.0)) stop = true;
+        }
+      }
+      smctot = smctot / dztot;
+      T fsat = M::pow(rmax(L(0.01), smctot / smcmax), L(4.0));
+      if (qinsrf > L(0.0)) {
+        runsrf = qinsrf * ((L(1.0) - fcr[0]) * fsat + fcr[0]);
+        qinfil = qinsrf - runsrf;
+      }
+    }
+    int niter = 1;
+    if (o.inf == 1) {
+      niter = 3;
+      if (qinfil * DT > c.dz[3] * smcmax) niter = niter * 2;
+    }
+    const T dtfine = DT / (T)niter;
+    T qdrain_save = L(0.0);
+    const T dwsat = (T)S.dwsat, dksat = (T)S.dksat;
+#pragma unroll 1
+    for (int it = 1; it <= niter; ++it) {
+      // srt: func.f90:6199-6305
+      T wdf[4], smx[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        if (o.inf == 1) {  // wdfcnd1
+          T factr = rmax(L(0.01), c.smc[k] / smcmax);
+          T expon = bexp + L(2.0);
+          wdf[k] = dwsat * M::pow(factr, expon);
+          wdf[k] = wdf[k] * (L(1.0) - fcr[k]);
+          expon = L(2.0) * bexp + L(3.0);
+          wcnd[k] = dksat * M::pow(factr, expon);
+          wcnd[k] = wcnd[k] * (L(1.0) - fcr[k]);
+          smx[k] = c.smc[k];
+        } else {  // wdfcnd2
+          T factr = rmax(L(0.01), c.sh2o[k] / smcmax);
+          T expon = bexp + L(2.0);
+          wdf[k] = dwsat * M::pow(factr, expon);
+          if (sicemax > L(0.0)) {
+            T vkwgt = L(1.0) / (L(1.0) + p3(L(500.0) * sicemax));
+            wdf[k] = vkwgt * wdf[k] + (L(1.0) - vkwgt) * dwsat * M::pow(L(0.2) / smcmax, expon);
+          }
+          expon = L(2.0) * bexp + L(3.0);
+          wcnd[k] = dksat * M::pow(factr, expon);
+          smx[k] = c.sh2o[k];
+        }
+      }
+      T ddz[4], denom[4], dsmdz[4], wflux[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        if (k == 0) {
+          denom[k] = -zsoil[k];
+          T temp1 = -zsoil[k + 1];
+          ddz[k] = L(2.0) / temp1;
+          dsmdz[k] = L(2.0) * (smx[k] - smx[k + 1]) / temp1;
+          wflux[k] = wdf[k] * dsmdz[k] + wcnd[k] - qinfil + etrani[k] + qseva;
+        } else if (k < 3) {
+          denom[k] = (zsoil[k - 1] - zsoil[k]);
+          T temp1 = (zsoil[k - 1] - zsoil[k + 1]);
+          ddz[k] = L(2.0) / temp1;
+          dsmdz[k] = L(2.0) * (smx[k] - smx[k + 1]) / temp1;
+          wflux[k] = wdf[k] * dsmdz[k] + wcnd[k] - wdf[k - 1] * dsmdz[k - 1] - wcnd[k - 1] +
+                     etrani[k];
+        } else {
+          denom[k] = (zsoil[k - 1] - zsoil[k]);
+          if (o.run == 1 || o.run == 2) qdrain = L(0.0);
+          if (o.run == 3) qdrain = (T)P.g.slope[c.slptyp - 1] * wcnd[k];
+          if (o.run == 4) qdrain = (L(1.0) - fcrmax) * wcnd[k];
+          ddz[k] = L(0.0);
+          dsmdz[k] = L(0.0);
+          wflux[k] = -(wdf[k - 1] * dsmdz[k - 1]) - wcnd[k - 1] + etrani[k] + qdrain;
+        }
+      }
+      T ai[4], bi[4], ci[4], rhstt[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        if (k == 0) {
+          ai[k] = L(0.0);
+          bi[k] = wdf[k] * ddz[k] / denom[k];
+          ci[k] = -bi[k];
+        } else if (k < 3) {
+          ai[k] = -wdf[k - 1] * ddz[k - 1] / denom[k];
+          ci[k] = -wdf[k] * ddz[k] / denom[k];
+          bi[k] = -(ai[k] + ci[k]);
+        } else {
+          ai[k] = -wdf[k - 1] * ddz[k - 1] / denom[k];
+          ci[k] = L(0.0);
+          bi[k] = -(ai[k] + ci[k]);
+        }
+        rhstt[k] = wflux[k] / (-denom[k]);
+      }
+      // sstep: func.f90:6308-6383
+      T ciin[4], rin[4], pp[4], del[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        rhstt[k] = rhstt[k] * dtfine;
+        ai[k] = ai[k] * dtfine;
+        bi[k] = L(1.0) + bi[k] * dtfine;
+        ci[k] = ci[k] * dtfine;
+        rin[k] = rhstt[k];
+        ciin[k] = ci[k];
+        pp[k] = L(0.);
+        del[k] = L(0.);
+      }
+      rosr12<T, 4>(pp, ai, bi, ciin, rin, del, 0);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) c.sh2o[k] = c.sh2o[k] + pp[k];
+      T wplus = L(0.0);
+#pragma unroll
+      for (int k = 3; k >= 1; --k) {
+        T ep = rmax(L(1.0E-4), smcmax - c.sice[k]);
+        wplus = rmax(c.sh2o[k] - ep, L(0.0)) * c.dz[k + 3];
+        c.sh2o[k] = rmin(ep, c.sh2o[k]);
+        c.sh2o[k - 1] = c.sh2o[k - 1] + wplus / c.dz[k + 2];
+      }
+      {
+        T ep = rmax(L(1.0E-4), smcmax - c.sice[0]);
+        wplus = rmax(c.sh2o[0] - ep, L(0.0)) * c.dz[3];
+        c.sh2o[0] = rmin(ep, c.sh2o[0]);
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) c.smc[k] = c.sh2o[k] + c.sice[k];
+      rsat = rsat + wplus;
+      qdrain_save = qdrain_save + qdrain;
+    }
+    qdrain = qdrain_save / (T)niter;
+    runsrf = runsrf * L(1000.0) + rsat * L(1000.0) / DT;
+    qdrain = qdrain * L(1000.0);
+    if (o.run == 2) {
+      T wtsub = L(0.0);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) wtsub = wtsub + wcnd[k] * c.dz[k + 3];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        T mh2o = runsub * DT * (wcnd[k] * c.dz[k + 3]) / wtsub;
+        c.sh2o[k] = c.sh2o[k] - mh2o / (c.dz[k + 3] * L(1000.0));
+      }
+    }
+    if (o.run != 1) {
+      T mliq[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) mliq[k] = c.sh2o[k] * c.dz[k + 3] * L(1000.0);
+      const T watmin = L(0.01);
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        T xs = (mliq[k] < L(0.0)) ? watmin - mliq[k] : L(0.0);
+        mliq[k] = mliq[k] + xs;
+        mliq[k + 1] = mliq[k + 1] - xs;
+      }
+      T xs = (mliq[3] < watmin) ? watmin - mliq[3] : L(0.0);
+      mliq[3] = mliq[3] + xs;
+      runsub = runsub - xs / DT;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) c.sh2o[k] = mliq[k] / (c.dz[k + 3] * L(1000.0));
+    }
+    if (o.run == 1) {
+      // groundwater: func.f90:6458-6639
+      const T ROUS = L(0.2), CMIC = L(0.20);
+      T dzmm[4], znode[4], mliq[4], epg[4], hk[4], smcg[4];
+      dzmm[0] = -zsoil[0] * L(1.0E3);
+#pragma unroll
+      for (int k = 1; k < 4; ++k) dzmm[k] = L(1.0E3) * (zsoil[k - 1] - zsoil[k]);
+      znode[0] = -zsoil[0] / L(2.0);
+#pragma unroll
+      for (int k = 1; k < 4; ++k) znode[k] = -zsoil[k - 1] + L(0.5) * (zsoil[k - 1] - zsoil[k]);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        smcg[k] = c.sh2o[k] + c.sice[k];
+        mliq[k] = c.sh2o[k] * dzmm[k];
+        epg[k] = rmax(L(0.01), smcmax - c.sice[k]);
+        hk[k] = L(1.0E3) * wcnd[k];
+      }
+      int iwt = 3;  // 0-based layer index above the water table
+      if (c.zwt <= -zsoil[1])
+        iwt = 0;
+      else if (c.zwt <= -zsoil[2])
+        iwt = 1;
+      else if (c.zwt <= -zsoil[3])
+        iwt = 2;
+      T qdis = (L(1.0) - fcrmax) * L(5.0) * M::exp(-(T)P.g.timean) * M::exp(-L(6.0) * (c.zwt - L(2.0)));
+      // S_NODE is real(8) in the reference (:6501): evaluate the matric potential in fp64
+      double s_node = (double)rmin(L(1.0), dget(smcg, iwt) / smcmax);
+      s_node = fmax(s_node, (double)0.01f);
+      T smpfz = (T)(-((double)(psisat * L(1000.0)) * ::pow(s_node, (double)(-bexp))));
+      smpfz = rmax(L(-120000.0), CMIC * smpfz);
+      T ka = dget(hk, iwt);
+      T znw = dget(znode, iwt);
+      T wh_zwt = -c.zwt * L(1.0E3);
+      T wh = smpfz - znw * L(1.0E3);
+      T qin = -ka * (wh_zwt - wh) / ((c.zwt - znw) * L(1.0E3));
+      qin = rmax(L(-10.0) / DT, rmin(L(10.0) / DT, qin));
+      c.wt = c.wt + (qin - qdis) * DT;
+      if (iwt == 3) {
+        c.wa = c.wa + (qin - qdis) * DT;
+        c.wt = c.wa;
+        c.zwt = (-zsoil[3] + L(25.0)) - c.wa / L(1000.0) / ROUS;
+        mliq[3] = mliq[3] - qin * DT;
+        mliq[3] = mliq[3] + rmax(L(0.0), c.wa - L(5000.0));
+        c.wa = rmin(c.wa, L(5000.0));
+      } else {
+        if (iwt == 2) {
+          c.zwt = -zsoil[3] - (c.wt - ROUS * L(1000.0) * L(25.0)) / (epg[3]) / L(1000.0);
+        } else {
+          T ws = L(0.0);
+#pragma unroll
+          for (int k = 1; k < 4; ++k)
+            if (k >= iwt + 2) ws = ws + epg[k] * dzmm[k];
+          c.zwt = -dget(zsoil, iwt + 1) - (c.wt - ROUS * L(1000.0) * L(25.0) - ws) /
+                                              (dget(epg, iwt + 1)) / L(1000.0);
+        }
+        T wtsub = L(0.0);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) wtsub = wtsub + hk[k] * dzmm[k];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) mliq[k] = mliq[k] - qdis * DT * hk[k] * dzmm[k] / wtsub;
+      }
+      c.zwt = rmax(L(1.5), c.zwt);
+      const T watmin = L(0.01);
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        T xs = (mliq[k] < L(0.0)) ? watmin - mliq[k] : L(0.0);
+        mliq[k] = mliq[k] + xs;
+        mliq[k + 1] = mliq[k + 1] - xs;
+      }
+      T xs = (mliq[3] < watmin) ? watmin - mliq[3] : L(0.0);
+      mliq[3] = mliq[3] + xs;
+      c.wa = c.wa - xs;
+      c.wt = c.wt - xs;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) c.sh2o[k] = mliq[k] / dzmm[k];
+      runsub = qdis;
+    }
+    if (o.run == 3 || o.run == 4) runsub = runsub + qdrain;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) c.smc[k] = c.sh2o[k] + c.sice[k];
+  }
+  runsub = runsub + snoflow;
+  // ===================== end water =====================
+
+  // carbon + co2flux (opt_veg 2|5): func.f90:6642-7025
+  T gpp = L(0.0), npp = L(0.0), nee = L(0.0);
+  if (o.veg == 2 || o.veg == 5) {
+    if (c.lutyp == P.g.iswater || c.lutyp == P.g.isbarren || c.lutyp == P.g.isice ||
+        c.lutyp == P.g.isurban) {
+      c.lai = c.sai = L(0.0);
+      c.lfmass = c.rtmass = c.stmass = c.wood = c.stblcp = c.fastcp = L(0.0);
+    } else {
+      T lapm = (T)V.sla / L(1000.0);
+      T wstres = L(1.0) - btran;
+      T wroot = L(0.0);
+      const T zr = -(nroot > 0 ? (T)zget(A.zsoil, nroot - 1) : L(1.0));
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        if (k < nroot) wroot = wroot + c.smc[k] / smcmax * c.dz[k + 3] / zr;
+      const T RTOVRC = L(2.0E-8), RSWOODC = L(3.0E-10), BF = L(0.90), WSTRC = L(100.0);
+      const T LAIMIN = L(0.05), XSAMIN = L(0.01);
+      T sapm = L(3.0) * L(0.001);
+      T lfmsmn = LAIMIN / lapm;
+      T stmsmn = XSAMIN / sapm;
+      T rf = (igs == L(0.0)) ? L(0.5) : L(1.0);
+      T fnf = rmin(c.foln / rmax(L(1.0E-06), (T)V.folnmx), L(1.0));
+      T tf = M::pow((T)V.arm, (c.tv - L(298.16)) / L(10.0));
+      T resp = (T)V.rmf25 * tf * fnf * c.lai * rf * (L(1.0) - wstres);
+      T rsleaf = rmin(c.lfmass / DT, resp * L(12.0E-6));
+      T rsroot = (T)V.rmr25 * (c.rtmass * L(1.0E-3)) * tf * rf * L(12.0E-6);
+      T rsstem = (T)V.rms25 * (c.stmass * L(1.0E-3)) * tf * rf * L(12.0E-6);
+      T rswood = RSWOODC * M::exp(L(0.08) * (c.tv - L(298.16))) * c.wood * (T)V.wdpool;
+      T carbfx = psn * L(12.0E-6);
+      T leafpt = M::exp(L(0.01) * (L(1.0) - M::exp(L(0.75) * c.lai)) * c.lai);
+      if (c.lutyp == P.g.isegblf) leafpt = M::exp(L(0.01) * (L(1.0) - M::exp(L(0.50) * c.lai)) * c.lai);
+      T nonlef = L(1.0) - leafpt;
+      T stempt = c.lai / L(10.0);
+      leafpt = leafpt - stempt;
+      T woodf = (c.wood > L(0.0))
+                    ? (L(1.0) - M::exp(-BF * ((T)V.wrrat * c.rtmass / c.wood)) / BF) * (T)V.wdpool
+                    : L(0.0);
+      T rootpt = nonlef * (L(1.0) - woodf);
+      T woodpt = nonlef * woodf;
+      T lftovr = (T)V.ltovrc * L(1.0E-6) * c.lfmass;
+      T sttovr = (T)V.ltovrc * L(1.0E-6) * c.stmass;
+      T rttovr = RTOVRC * c.rtmass;
+      T wdtovr = L(9.5E-10) * c.wood;
+      T sc = M::exp(L(-0.3) * rmax(L(0.0), c.tv - (T)V.tdlef)) * (c.lfmass / L(120.0));
+      T sd = M::exp((wstres - L(1.0)) * WSTRC);
+      T dielf = c.lfmass * L(1.0E-6) * ((T)V.dilefw * sd + (T)V.dilefc * sc);
+      T diest = c.stmass * L(1.0E-6) * ((T)V.dilefw * sd + (T)V.dilefc * sc);
+      T fragr = (T)V.fragr;
+      T grleaf = rmax(L(0.0), fragr * (leafpt * carbfx - rsleaf));
+      T grstem = rmax(L(0.0), fragr * (stempt * carbfx - rsstem));
+      T grroot = rmax(L(0.0), fragr * (rootpt * carbfx - rsroot));
+      T grwood = rmax(L(0.0), fragr * (woodpt * carbfx - rswood));
+      T addnpplf = rmax(L(0.), leafpt * carbfx - grleaf - rsleaf);
+      T addnppst = rmax(L(0.), stempt * carbfx - grstem - rsstem);
+      if (c.tv < (T)V.tmin) addnpplf = L(0.0);
+      if (c.tv < (T)V.tmin) addnppst = L(0.0);
+      T lfdel = (c.lfmass - lfmsmn) / DT;
+      T stdel = (c.stmass - stmsmn) / DT;
+      dielf = rmin(dielf, lfdel + addnpplf - lftovr);
+      diest = rmin(diest, stdel + addnppst - sttovr);
+      T nppl = rmax(addnpplf, -lfdel);
+      T npps = rmax(addnppst, -stdel);
+      T nppr = rootpt * carbfx - rsroot - grroot;
+      T nppw = woodpt * carbfx - rswood - grwood;
+      c.lfmass = c.lfmass + (nppl - lftovr - dielf) * DT;
+      c.stmass = c.stmass + (npps - sttovr - diest) * DT;
+      c.rtmass = c.rtmass + (nppr - rttovr) * DT;
+      if (c.rtmass < L(0.0)) {
+        rttovr = nppr;
+        c.rtmass = L(0.0);
+      }
+      c.wood = (c.wood + (nppw - wdtovr) * DT) * (T)V.wdpool;
+      c.fastcp = c.fastcp + (rttovr + lftovr + sttovr + wdtovr + dielf) * DT;
+      T fst = M::exp2((c.stc[3] - L(283.16)) / L(10.0));
+      T fsw = wroot / (L(0.20) + wroot) * L(0.23) / (L(0.23) + wroot);
+      T rssoil = fsw * fst * (T)V.mrp * rmax(L(0.0), c.fastcp * L(1.0E-3)) * L(12.0E-6);
+      T stablc = L(0.1) * rssoil;
+      c.fastcp = c.fastcp - (rssoil + stablc) * DT;
+      c.stblcp = c.stblcp + stablc * DT;
+      gpp = carbfx;
+      npp = nppl + nppw + nppr;
+      T autors = rsroot + rswood + rsleaf + grleaf + grroot + grwood;
+      T heters = rssoil;
+      nee = (autors + heters - gpp) * L(44.0) / L(12.0);
+      c.lai = rmax(c.lfmass * lapm, LAIMIN);
+      c.sai = rmax(c.stmass * sapm, XSAMIN);
+    }
+  }
+
+  // error(): energy / shortwave balance checks (func.f90:633-732)
+  if (fabs(swdown - (fsa + fsr)) > L(0.01)) c.status |= NMP_ST_ERRSW;
+  if (fabs(sav + sag - (fira + fsh + fcev + fgev + fctr + ssoil)) > L(0.01))
+    c.status |= NMP_ST_ERRENG;
+  // urban QSFC (:459-463)
+  if (c.lutyp == P.g.isurban) {
+    T qfx = etran + ecan + edir;
+    c.qsfc = (qfx / rhoair * c.ch) + qair;
+    q2b = c.qsfc;
+  }
+  if (c.snowh <= L(1.0E-6) || c.sneqv <= L(1.0E-3)) {
+    c.snowh = L(0.0);
+    c.sneqv = L(0.0);
+  }
+  T albedo = (swdown != L(0.0)) ? fsr / swdown : L(-999.9);
+
+  dout[NMP_D_FSA] = fsa; dout[NMP_D_FSR] = fsr; dout[NMP_D_FIRA] = fira; dout[NMP_D_FSH] = fsh;
+  dout[NMP_D_SSOIL] = ssoil; dout[NMP_D_FCEV] = fcev; dout[NMP_D_FGEV] = fgev;
+  dout[NMP_D_FCTR] = fctr; dout[NMP_D_ECAN] = ecan; dout[NMP_D_ETRAN] = etran;
+  dout[NMP_D_EDIR] = edir; dout[NMP_D_TRAD] = trad; dout[NMP_D_TGB] = tgb; dout[NMP_D_TGV] = tgv;
+  dout[NMP_D_T2MV] = t2mv; dout[NMP_D_T2MB] = t2mb; dout[NMP_D_Q2V] = q2v; dout[NMP_D_Q2B] = q2b;
+  dout[NMP_D_RUNSRF] = runsrf; dout[NMP_D_RUNSUB] = runsub; dout[NMP_D_APAR] = apar;
+  dout[NMP_D_PSN] = psn; dout[NMP_D_SAV] = sav; dout[NMP_D_SAG] = sag; dout[NMP_D_FSNO] = fsno;
+  dout[NMP_D_NEE] = nee; dout[NMP_D_GPP] = gpp; dout[NMP_D_NPP] = npp; dout[NMP_D_FVEG] = fveg;
+  dout[NMP_D_ALBEDO] = albedo; dout[NMP_D_QSNBOT] = qsnbot; dout[NMP_D_PONDING] = ponding;
+  dout[NMP_D_PONDING1] = ponding1; dout[NMP_D_PONDING2] = ponding2; dout[NMP_D_RSSUN] = rssun;
+  dout[NMP_D_RSSHA] = rssha; dout[NMP_D_BGAP] = bgap; dout[NMP_D_WGAP] = wgap;
+  dout[NMP_D_CHV] = chv; dout[NMP_D_CHB] = chb; dout[NMP_D_EMISSI] = emissi;
+  dout[NMP_D_SHG] = shg; dout[NMP_D_SHC] = shc; dout[NMP_D_SHB] = shb; dout[NMP_D_EVG] = evg;
+  dout[NMP_D_EVB] = evb; dout[NMP_D_GHV] = ghv; dout[NMP_D_GHB] = ghb; dout[NMP_D_IRG] = irg;
+  dout[NMP_D_IRC] = irc; dout[NMP_D_IRB] = irb; dout[NMP_D_TR] = tr; dout[NMP_D_EVC] = evc;
+  dout[NMP_D_CHLEAF] = chleaf; dout[NMP_D_CHUC] = chuc; dout[NMP_D_CHV2] = chv2;
+  dout[NMP_D_CHB2] = chb2; dout[NMP_D_FPICE] = fpice;
+  t2m_out = t2m;
+}
+
+// ---------------------------------------------------------------------------
+template <class T, bool R>
+__global__ __launch_bounds__(256) void sflx_step_kernel(const DevParams* __restrict__ gparams,
+                                                          KArgs<T> a) {
+  __shared__ __attribute__((aligned(16))) DevParams sp;
+  {
+    const int4* src = reinterpret_cast<const int4*>(gparams);
+    int4* dst = reinterpret_cast<int4*>(&sp);
+    constexpr int NW = sizeof(DevParams) / sizeof(int4);
+    for (int i = threadIdx.x; i < NW; i += blockDim.x) dst[i] = src[i];
+  }
+  __syncthreads();
+  const int64_t c0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c0 >= a.ncol) return;
+  const int64_t ld = a.ld;
+  Col<T> c;
+  const T* st = a.state + c0;
+#pragma unroll
+  for (int k = 0; k < 7; ++k) {
+    c.stc[k] = st[(NMP_S_STC + k) * ld];
+    c.zsnso[k] = st[(NMP_S_ZSNSO + k) * ld];
+  }
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    c.snice[k] = st[(NMP_S_SNICE + k) * ld];
+    c.snliq[k] = st[(NMP_S_SNLIQ + k) * ld];
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    c.sh2o[k] = st[(NMP_S_SH2O + k) * ld];
+    c.smc[k] = st[(NMP_S_SMC + k) * ld];
+  }
+  c.tv = st[NMP_S_TV * ld]; c.tg = st[NMP_S_TG * ld]; c.tah = st[NMP_S_TAH * ld];
+  c.eah = st[NMP_S_EAH * ld]; c.fwet = st[NMP_S_FWET * ld]; c.canliq = st[NMP_S_CANLIQ * ld];
+  c.canice = st[NMP_S_CANICE * ld]; c.qsfc = st[NMP_S_QSFC * ld]; c.snowh = st[NMP_S_SNOWH * ld];
+  c.sneqv = st[NMP_S_SNEQV * ld]; c.sneqvo = st[NMP_S_SNEQVO * ld];
+  c.albold = st[NMP_S_ALBOLD * ld]; c.tauss = st[NMP_S_TAUSS * ld];
+  c.qsnow = st[NMP_S_QSNOW * ld]; c.zwt = st[NMP_S_ZWT * ld]; c.wa = st[NMP_S_WA * ld];
+  c.wt = st[NMP_S_WT * ld]; c.wslake = st[NMP_S_WSLAKE * ld]; c.lai = st[NMP_S_LAI * ld];
+  c.sai = st[NMP_S_SAI * ld]; c.lfmass = st[NMP_S_LFMASS * ld]; c.rtmass = st[NMP_S_RTMASS * ld];
+  c.stmass = st[NMP_S_STMASS * ld]; c.wood = st[NMP_S_WOOD * ld]; c.stblcp = st[NMP_S_STBLCP * ld];
+  c.fastcp = st[NMP_S_FASTCP * ld]; c.cm = st[NMP_S_CM * ld]; c.ch = st[NMP_S_CH * ld];
+  c.isnow = a.isnow[c0];
+  const T* sf = a.static_f + c0;
+  c.lat = sf[NMP_F_LAT * ld]; c.zref = sf[NMP_F_ZLVL * ld]; c.shdfac = sf[NMP_F_SHDFAC * ld];
+  c.shdmax = sf[NMP_F_SHDMAX * ld]; c.tbot = sf[NMP_F_TBOT * ld]; c.foln = sf[NMP_F_FOLN * ld];
+  const int32_t* si = a.static_i + c0;
+  c.lutyp = si[NMP_I_VEGTYP * ld]; c.sltyp = si[NMP_I_SOILTYP * ld];
+  c.slptyp = si[NMP_I_SLOPETYP * ld]; c.isc = si[NMP_I_SOILCOLOR * ld];
+  c.ist = si[NMP_I_IST * ld]; c.ice = si[NMP_I_ICE * ld];
+  const T* fc = a.forcing + c0;
+  c.sfctmp = fc[NMP_A_SFCTMP * ld]; c.sfcprs = fc[NMP_A_SFCPRS * ld]; c.psfc = fc[NMP_A_PSFC * ld];
+  c.uu = fc[NMP_A_UU * ld]; c.vv = fc[NMP_A_VV * ld]; c.q2 = fc[NMP_A_Q2 * ld];
+  c.soldn = fc[NMP_A_SOLDN * ld]; c.lwdn = fc[NMP_A_LWDN * ld]; c.prcp = fc[NMP_A_PRCP * ld];
+  c.cosz = fc[NMP_A_COSZ * ld]; c.co2air = fc[NMP_A_CO2AIR * ld]; c.o2air = fc[NMP_A_O2AIR * ld];
+  c.status = 0;
+
+  T d[NMP_NDIAG_FULL];
+  T t2m;
+  sflx_column<T, R>(sp, a, c, d, t2m);
+
+  T* so = a.state + c0;
+#pragma unroll
+  for (int k = 0; k < 7; ++k) {
+    so[(NMP_S_STC + k) * ld] = c.stc[k];
+    so[(NMP_S_ZSNSO + k) * ld] = c.zsnso[k];
+  }
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    so[(NMP_S_SNICE + k) * ld] = c.snice[k];
+    so[(NMP_S_SNLIQ + k) * ld] = c.snliq[k];
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    so[(NMP_S_SH2O + k) * ld] = c.sh2o[k];
+    so[(NMP_S_SMC + k) * ld] = c.smc[k];
+  }
+  so[NMP_S_TV * ld] = c.tv; so[NMP_S_TG * ld] = c.tg; so[NMP_S_TAH * ld] = c.tah;
+  so[NMP_S_EAH * ld] = c.eah; so[NMP_S_FWET * ld] = c.fwet; so[NMP_S_CANLIQ * ld] = c.canliq;
+  so[NMP_S_CANICE * ld] = c.canice; so[NMP_S_QSFC * ld] = c.qsfc; so[NMP_S_SNOWH * ld] = c.snowh;
+  so[NMP_S_SNEQV * ld] = c.sneqv; so[NMP_S_SNEQVO * ld] = c.sneqvo;
+  so[NMP_S_ALBOLD * ld] = c.albold; so[NMP_S_TAUSS * ld] = c.tauss;
+  so[NMP_S_QSNOW * ld] = c.qsnow; so[NMP_S_ZWT * ld] = c.zwt; so[NMP_S_WA * ld] = c.wa;
+  so[NMP_S_WT * ld] = c.wt; so[NMP_S_WSLAKE * ld] = c.wslake; so[NMP_S_LAI * ld] = c.lai;
+  so[NMP_S_SAI * ld] = c.sai; so[NMP_S_LFMASS * ld] = c.lfmass; so[NMP_S_RTMASS * ld] = c.rtmass;
+  so[NMP_S_STMASS * ld] = c.stmass; so[NMP_S_WOOD * ld] = c.wood; so[NMP_S_STBLCP * ld] = c.stblcp;
+  so[NMP_S_FASTCP * ld] = c.fastcp; so[NMP_S_CM * ld] = c.cm; so[NMP_S_CH * ld] = c.ch;
+  a.isnow[c0] = c.isnow;
+  if (c.status != 0) a.status[c0] |= c.status;
+  if (a.diag_level == NMP_DIAG_FULL) {
+    T* dg = a.diag + c0;
+#pragma unroll
+    for (int k = 0; k < NMP_NDIAG_FULL; ++k) dg[k * ld] = d[k];
+  } else if (a.diag_level == NMP_DIAG_OUT) {
+    T* dg = a.diag + c0;
+    dg[NMP_O_FSA * ld] = d[NMP_D_FSA]; dg[NMP_O_FSR * ld] = d[NMP_D_FSR];
+    dg[NMP_O_FIRA * ld] = d[NMP_D_FIRA]; dg[NMP_O_FSH * ld] = d[NMP_D_FSH];
+    dg[NMP_O_SSOIL * ld] = d[NMP_D_SSOIL]; dg[NMP_O_FCEV * ld] = d[NMP_D_FCEV];
+    dg[NMP_O_FGEV * ld] = d[NMP_D_FGEV]; dg[NMP_O_FCTR * ld] = d[NMP_D_FCTR];
+    dg[NMP_O_ECAN * ld] = d[NMP_D_ECAN]; dg[NMP_O_ETRAN * ld] = d[NMP_D_ETRAN];
+    dg[NMP_O_EDIR * ld] = d[NMP_D_EDIR]; dg[NMP_O_TRAD * ld] = d[NMP_D_TRAD];
+    dg[NMP_O_RUNSRF * ld] = d[NMP_D_RUNSRF]; dg[NMP_O_RUNSUB * ld] = d[NMP_D_RUNSUB];
+    dg[NMP_O_T2M * ld] = t2m; dg[NMP_O_ALBEDO * ld] = d[NMP_D_ALBEDO];
+  }
+}
+
+// launch wrapper (one instantiation per precision / math policy)
+template <class T, bool R>
+hipError_t launch_sflx(const DevParams* dparams, const KArgs<T>& a, hipStream_t stream) {
+  const int block = 256;
+  const int64_t grid = (a.ncol + block - 1) / block;
+  if (grid == 0) return hipSuccess;
+  hipLaunchKernelGGL((sflx_step_kernel<T, R>), dim3((unsigned)grid), dim3(block), 0, stream,
+                     dparams, a);
+  return hipGetLastError();
+}
+
+template hipError_t launch_sflx<float, true>(const DevParams*, const KArgs<float>&, hipStream_t);
+template hipError_t launch_sflx<float, false>(const DevParams*, const KArgs<float>&, hipStream_t);
+template hipError_t launch_sflx<double, false>(const DevParams*, const KArgs<double>&, hipStream_t);
+
+}  // namespace nmp

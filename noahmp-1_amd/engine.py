@@ -1,0 +1,142 @@
+"""Python front end of the HIP column engine (drop-in for core/module_noahmp_engine.f90).
+
+`Engine` owns the engine handle (tables on the device + options); column data
+are caller-owned torch tensors on the engine's GPU in field-major SoA layout
+(see layout.py / include/noahmp_engine.h).  `ColumnState` bundles the arrays
+of one column set.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+
+import numpy as np
+import torch
+
+from . import layout as L
+from . import lib as _lib
+from .params import Params
+
+MATH_REF, MATH_FAST = 0, 1
+
+
+def _ptr(t):
+    return C.c_void_p(t.data_ptr()) if t is not None else C.c_void_p(0)
+
+
+@dataclass
+class ColumnState:
+    """Device-resident SoA arrays for ncol columns (leading dimension ncol)."""
+    state: torch.Tensor     # (56, n) real
+    isnow: torch.Tensor     # (n,) int32
+    static_f: torch.Tensor  # (6, n) real
+    static_i: torch.Tensor  # (6, n) int32
+    status: torch.Tensor    # (n,) int32
+
+    @property
+    def ncol(self) -> int:
+        return int(self.isnow.shape[0])
+
+    @classmethod
+    def from_host(cls, cols, device, dtype=torch.float32) -> "ColumnState":
+        """From a cases.ColumnSet (numpy SoA)."""
+        dev = torch.device(device)
+        return cls(
+            state=torch.as_tensor(np.ascontiguousarray(cols.state), device=dev).to(dtype).contiguous(),
+            isnow=torch.as_tensor(np.ascontiguousarray(cols.isnow, np.int32), device=dev),
+            static_f=torch.as_tensor(np.ascontiguousarray(cols.static_f), device=dev).to(dtype).contiguous(),
+            static_i=torch.as_tensor(np.ascontiguousarray(cols.static_i, np.int32), device=dev),
+            status=torch.zeros(cols.isnow.shape[0], dtype=torch.int32, device=dev),
+        )
+
+    def narrow(self, start: int, length: int) -> "ColumnState":
+        """A contiguous copy of a column range (for sharding)."""
+        return ColumnState(self.state[:, start:start + length].contiguous(),
+                           self.isnow[start:start + length].contiguous(),
+                           self.static_f[:, start:start + length].contiguous(),
+                           self.static_i[:, start:start + length].contiguous(),
+                           self.status[start:start + length].contiguous())
+
+
+class Engine:
+    """One engine per device: noahmp_init + *_readptable + noahmp_set_options."""
+
+    def __init__(self, params: Params | None = None, options: dict | None = None,
+                 device: int = 0, precision: int = 4, math: int | str = MATH_REF):
+        self._lib = _lib.load()
+        self.params = params if params is not None else Params.builtin()
+        opts = dict(L.CASE_NML_OPTIONS)
+        if options:
+            opts.update(options)
+        self.options = opts
+        self.device = int(device)
+        self.precision = int(precision)
+        self.dtype = torch.float32 if precision == 4 else torch.float64
+        o = _lib.NmpOptions(*[int(opts[k]) for k in _lib.NMP_OPTION_FIELDS])
+        h = C.c_void_p()
+        _lib.check(self._lib.nmp_init(C.byref(self.params.struct), C.byref(o), self.device,
+                                      self.precision, C.byref(h)), "nmp_init")
+        self._h = h
+        if isinstance(math, str):
+            math = MATH_FAST if math == "fast" else MATH_REF
+        self.set_math(math)
+
+    def set_math(self, mode: int):
+        _lib.check(self._lib.nmp_set_math(self._h, int(mode)), "nmp_set_math")
+        self.math = int(mode)
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._lib.nmp_finalize(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ------------------------------------------------------------------------
+    def _check_cols(self, cs: ColumnState, forcing: torch.Tensor):
+        n = cs.ncol
+        assert cs.state.shape == (L.NSTATE, n) and cs.state.dtype == self.dtype
+        assert cs.state.is_contiguous() and cs.static_f.is_contiguous()
+        assert cs.static_f.shape == (L.NSTATIC_F, n) and cs.static_f.dtype == self.dtype
+        assert cs.static_i.shape == (L.NSTATIC_I, n) and cs.static_i.dtype == torch.int32
+        assert cs.isnow.dtype == torch.int32 and cs.status.dtype == torch.int32
+        assert forcing.shape[-2:] == (L.NFORCING, n) and forcing.dtype == self.dtype
+        assert forcing.is_contiguous()
+        for t in (cs.state, cs.isnow, cs.static_f, cs.static_i, cs.status, forcing):
+            assert t.device.type == "cuda" and t.device.index == self.device, t.device
+
+    def step(self, cs: ColumnState, forcing: torch.Tensor, zsoil, dt: float, julian: float,
+             yearlen: int, diag: torch.Tensor | None = None, diag_level: int = L.DIAG_NONE,
+             stream=None):
+        """One noahmp_sflx step for every column (enqueued on `stream`)."""
+        self._check_cols(cs, forcing)
+        n = cs.ncol
+        if diag_level != L.DIAG_NONE:
+            nd = L.NDIAG_FULL if diag_level == L.DIAG_FULL_LEVEL else L.NDIAG_OUT
+            assert diag is not None and diag.shape == (nd, n) and diag.dtype == self.dtype
+        zs = (C.c_float * 4)(*[float(z) for z in zsoil])
+        s = stream if stream is not None else torch.cuda.current_stream(self.device)
+        _lib.check(self._lib.nmp_step(self._h, n, n, zs, float(dt), float(julian), int(yearlen),
+                                      _ptr(cs.state), _ptr(cs.isnow), _ptr(cs.static_f),
+                                      _ptr(cs.static_i), _ptr(forcing), _ptr(diag), int(diag_level),
+                                      _ptr(cs.status), C.c_void_p(s.cuda_stream)), "nmp_step")
+
+    def run(self, cs: ColumnState, forcings: torch.Tensor, zsoil, dt: float, julian0: float,
+            yearlen: int, nsteps: int, diag: torch.Tensor | None = None,
+            diag_level: int = L.DIAG_NONE, stream=None):
+        """nsteps steps cycling through forcings[(period, 12, n)] (last-step diagnostics)."""
+        n = cs.ncol
+        assert forcings.dim() == 3
+        self._check_cols(cs, forcings[0])
+        zs = (C.c_float * 4)(*[float(z) for z in zsoil])
+        s = stream if stream is not None else torch.cuda.current_stream(self.device)
+        _lib.check(self._lib.nmp_run(self._h, n, n, zs, float(dt), float(julian0), int(yearlen),
+                                     int(nsteps), _ptr(cs.state), _ptr(cs.isnow),
+                                     _ptr(cs.static_f), _ptr(cs.static_i), _ptr(forcings),
+                                     L.NFORCING * n, forcings.shape[0], _ptr(diag),
+                                     int(diag_level), _ptr(cs.status),
+                                     C.c_void_p(s.cuda_stream)), "nmp_run")
