@@ -1,0 +1,203 @@
+#!/usr/bin/env python3
+"""Headline benchmark: land-column time steps per second (noahmp_sflx on MI355X).
+
+Workload (BASELINE.json configs[2], "config #3"): 1,048,576 synthetic columns
+per GPU, 4 soil + 3 snow layers, mixed vegetated USGS types / soil types /
+soil colours, ISNOW uniform in {0,-1,-2,-3}, dynamic vegetation off
+(case.nml options), fp32.  One bench step = one noahmp_sflx time step of
+every column (one kernel launch, state resident in HBM); every
+--out-every'th step also writes the 16 output diagnostics and, for N > 1,
+all-gathers them across ranks (RCCL over xGMI) on a side stream.
+
+Multi-GPU: one process per GPU (torchrun), columns statically sharded with
+no data-path collective other than that diagnostics all-gather; per-GPU work
+is fixed (weak scaling).
+
+Prints one JSON line (rank 0) with the driver contract fields plus
+`roofline` (dominant kernel vs HBM peak) and `cpu_baseline`.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+
+import noahmp_pkg  # noqa: E402,F401
+from noahmp_amd import cases, layout as L  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E, /opt/skills/guides/MI355X_MICROARCH.md
+METRIC = BASELINE_METRIC = "land-columns·timesteps/sec at 4 soil + 3 snow layers, 1/2/4/8 MI355X"
+
+
+def bytes_per_colstep(precision: int, diag: bool) -> int:
+    """Algorithmic HBM bytes per column-step: state read+write
+    (56 reals + int32 ISNOW), static 6 reals + 6 int32, forcing 12 reals,
+    + 16 output diagnostics on output steps.  fp32: 552 (+64)."""
+    s = precision
+    b = 2 * (56 * s + 4) + 6 * s + 6 * 4 + 12 * s
+    return b + (16 * s if diag else 0)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=48)
+    ap.add_argument("--warmup", type=int, default=4)
+    ap.add_argument("--ncol", type=int, default=1 << 20, help="columns per GPU")
+    ap.add_argument("--precision", type=int, default=4, choices=(4, 8))
+    ap.add_argument("--math", default="ref", choices=("ref", "fast"))
+    ap.add_argument("--dt", type=float, default=1800.0)
+    ap.add_argument("--out-every", type=int, default=2, help="output (diag) step interval")
+    ap.add_argument("--period", type=int, default=48, help="resident forcing slices (cycled)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-steps", type=int, default=32)
+    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic.json"),
+                    help="PMC-measured HBM bytes per launch (written by tools/pmc_traffic.py)")
+    return ap.parse_args()
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    assert world == a.gpus or world == 1, "launch N>1 with torchrun --nproc-per-node N"
+
+    from noahmp_amd.params import Params
+    P = Params.builtin("STAS", "USGS")
+    pdict = P.as_dict()
+    options = L.options_tuple(L.CASE_NML_OPTIONS)
+    julian0, yearlen, seed = 180.0, 366, 1000 + rank
+    cols = cases.make_columns(a.ncol, "mixed", pdict, seed=seed, julian=julian0)
+
+    # ---- CPU baseline (rank 0, N=1), BEFORE anything touches the GPU ------
+    cpu = None
+    if world == 1 and not a.no_cpu_baseline:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        try:
+            import cpu_baseline
+            cpu = cpu_baseline.measure(cols, pdict, options, cases.CASE_NML_ZSOIL, a.dt, julian0,
+                                       yearlen, seed, a.period, nsteps=a.cpu_steps)
+        except Exception as e:  # the baseline is reported, never required
+            cpu = {"value": None, "error": repr(e)[:200]}
+
+    import torch
+    import torch.distributed as dist
+    from noahmp_amd.engine import ColumnState, Engine
+
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+    dtype = torch.float32 if a.precision == 4 else torch.float64
+    eng = Engine(P, L.CASE_NML_OPTIONS, device=local, precision=a.precision, math=a.math)
+    cs = ColumnState.from_host(cols, dev, dtype)
+    n = cs.ncol
+    F = torch.empty((a.period, L.NFORCING, n), dtype=dtype, device=dev)
+    for s in range(a.period):
+        F[s].copy_(torch.from_numpy(cases.forcing_step(
+            cols, julian0 + s * a.dt / 86400.0, yearlen, s, seed=seed)))
+    diag = [torch.zeros((L.NDIAG_OUT, n), dtype=dtype, device=dev) for _ in range(2)]
+    gathered = [torch.empty((world * L.NDIAG_OUT, n), dtype=dtype, device=dev) for _ in range(2)] \
+        if world > 1 else None
+    pending = [None, None]
+    compute = torch.cuda.Stream(dev)
+    comm = torch.cuda.Stream(dev) if world > 1 else None
+    del cols
+
+    def step(k, ev=None):
+        """Bench step k on the compute stream (+ async diag all-gather on output steps)."""
+        out = (k + 1) % a.out_every == 0
+        b = (k // a.out_every) % 2
+        with torch.cuda.stream(compute):
+            if out and pending[b] is not None:
+                pending[b].wait()  # the previous gather from this buffer is done
+                pending[b] = None
+            if ev is not None:
+                ev[0].record(compute)
+            eng.step(cs, F[k % a.period], cases.CASE_NML_ZSOIL, a.dt,
+                     julian0 + k * a.dt / 86400.0, yearlen, diag[b] if out else None,
+                     L.DIAG_OUT_LEVEL if out else L.DIAG_NONE, stream=compute)
+            if ev is not None:
+                ev[1].record(compute)
+        if out and world > 1:
+            comm.wait_stream(compute)
+            with torch.cuda.stream(comm):
+                pending[b] = dist.all_gather_into_tensor(gathered[b], diag[b], async_op=True)
+        return out
+
+    for k in range(a.warmup):
+        step(k)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+           for _ in range(a.steps)]
+    outs = 0
+    t0 = time.perf_counter()
+    for k in range(a.steps):
+        outs += step(a.warmup + k, evs[k])
+    for p in pending:
+        if p is not None:
+            p.wait()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    kern_ms = float(np.mean([e0.elapsed_time(e1) for e0, e1 in evs]))
+    st_bad = int((cs.status != 0).sum().item())
+    finite = bool(torch.isfinite(cs.state[L.s("STC")]).all().item())
+    if world > 1:
+        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, kern_ms = float(t[0]), float(t[1])
+
+    if rank == 0:
+        colsteps = world * n * a.steps
+        value = colsteps / elapsed
+        # algorithmic bytes per launch, averaged over plain and output steps
+        bpl = n * (bytes_per_colstep(a.precision, False) * (a.steps - outs)
+                   + bytes_per_colstep(a.precision, True) * outs) / a.steps
+        achieved = bpl / (kern_ms * 1e-3) / 1e9
+        traffic = None
+        if os.path.exists(a.traffic):
+            with open(a.traffic) as f:
+                tj = json.load(f)
+            if tj.get("ncol") == n and tj.get("precision") == a.precision and \
+                    tj.get("math") == a.math:
+                traffic = tj.get("bytes_per_launch")
+        line = {
+            "metric": METRIC, "value": value, "unit": "column-steps/s", "n_gpus": world,
+            "steps": a.steps, "warmup": a.warmup, "ms_per_step": elapsed * 1e3 / a.steps,
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": "f32" if a.precision == 4 else "f64",
+            "data": "synthetic (seeded mixed USGS/STAS columns, diurnal forcing; no dataset)",
+            "config": {"workload": "config #3: 1,048,576 columns/GPU, 4 soil + 3 snow layers, "
+                                   "dynamic_veg off, case.nml options" if n == 1 << 20 else
+                       f"{n} columns/GPU, 4 soil + 3 snow layers", "ncol_per_gpu": n,
+                       "ncol_total": world * n, "dt_s": a.dt, "out_every": a.out_every,
+                       "math": a.math, "parallelism": f"column-shard x{world}"},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "kernel": "sflx_step_kernel", "kernel_ms": kern_ms,
+                         "bytes_per_launch": bpl},
+            "cpu_baseline": cpu,
+            "checks": {"status_nonzero_cols": st_bad, "stc_finite": finite},
+        }
+        print(json.dumps(line), flush=True)
+    eng.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1121,8 +1121,8 @@ static void rosr12(real* Pp, const real* A, const real* B, real* C, const real* 
 /* tsnosoi + hrt + hstep: func.f90:3987-4237 */
 static void tsnosoi(ctx_t* X, int ISNOW, real TBOT, const real* ZSNSO, real SSOIL, const real* DF,
                     const real* HCPCT, real ZBOT, real DT, real snowh, real* STC) {
-  real AIb[7], BIb[7], CIb[7], RHSb[7], DDZb[7], DENOMb[7], DTSDZb[7], EFLUXb[7], CIINb[7],
-      RHSINb[7];
+  real AIb[7] = {0}, BIb[7] = {0}, CIb[7] = {0}, RHSb[7] = {0}, DDZb[7], DENOMb[7], DTSDZb[7], EFLUXb[7], CIINb[7],
+      RHSINb[7] = {0};
   real *AI = AIb + 2, *BI = BIb + 2, *CI = CIb + 2, *RHSTS = RHSb + 2, *DDZ = DDZb + 2,
        *DENOM = DENOMb + 2, *DTSDZ = DTSDZb + 2, *EFLUX = EFLUXb + 2, *CIIN = CIINb + 2,
        *RHSTSIN = RHSINb + 2;

@@ -1,0 +1,169 @@
+"""C-ABI surface and host logic (no GPU compute).
+
+- every entry point include/noahmp_engine.h declares is exported by the built
+  library and bound in lib.py;
+- layout.py offsets == the header enums;
+- error paths that return before touching a device;
+- nmp_state_from_aos maps noahmp_state_t records (core/module_noahmp_type.f90:10-42);
+- time manager / synthetic case generators."""
+import ctypes as C
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+from noahmp_amd import cases, layout as L, lib as _lib, timeman
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "noahmp_engine.h")
+
+
+def _header():
+    with open(HEADER) as f:
+        return f.read()
+
+
+def _enum_values(text):
+    """NAME -> value for every NMP_* enumerator (implicit increments included)."""
+    out = {}
+    for body in re.findall(r"enum\s*\{(.*?)\}", text, re.S):
+        body = re.sub(r"/\*.*?\*/", "", body, flags=re.S)
+        nxt = 0
+        for item in body.split(","):
+            item = item.strip()
+            if not item:
+                continue
+            m = re.match(r"(\w+)\s*(?:=\s*(-?\d+))?$", item)
+            assert m, item
+            v = int(m.group(2)) if m.group(2) is not None else nxt
+            out[m.group(1)] = v
+            nxt = v + 1
+    return out
+
+
+def test_header_functions_exported(engine_lib):
+    decl = set(re.findall(r"^\s*(?:int|void|const char\*)\s+(nmp_\w+)\s*\(", _header(), re.M))
+    assert decl == set(_lib.EXPORTED_SYMBOLS)
+    nm = subprocess.run(["nm", "-D", "--defined-only", _lib.library_path()], capture_output=True,
+                        text=True, check=True).stdout
+    exported = set(re.findall(r"\bT (nmp_\w+)$", nm, re.M))
+    assert decl <= exported, decl - exported
+    for name in decl:
+        assert getattr(engine_lib, name) is not None
+
+
+def test_layout_matches_header():
+    e = _enum_values(_header())
+    for name, (off, _w) in L.STATE_OFF.items():
+        assert e[f"NMP_S_{name}"] == off, name
+    assert e["NMP_NSTATE"] == L.NSTATE
+    for i, n in enumerate(L.STATIC_F):
+        assert e[f"NMP_F_{n}"] == i
+    for i, n in enumerate(L.STATIC_I):
+        assert e[f"NMP_I_{n}"] == i
+    for i, n in enumerate(L.FORCING):
+        assert e[f"NMP_A_{n}"] == i
+    for i, n in enumerate(L.DIAG_FULL):
+        assert e[f"NMP_D_{n}"] == i
+    for i, n in enumerate(L.DIAG_OUT):
+        assert e[f"NMP_O_{n}"] == i
+    assert (e["NMP_DIAG_NONE"], e["NMP_DIAG_OUT"], e["NMP_DIAG_FULL"]) == (
+        L.DIAG_NONE, L.DIAG_OUT_LEVEL, L.DIAG_FULL_LEVEL)
+    for k in ("ERRSW", "ERRENG", "FIRE", "HCAN", "ZLVL", "FLERCH", "OPTVEG", "STOP"):
+        assert e[f"NMP_ST_{k}"] == getattr(L, f"ST_{k}")
+
+
+def test_params_struct_size():
+    import ref  # oracle/ref.py: the reference dump order == struct order
+    assert C.sizeof(_lib.NmpParams) == 4 * (ref.NPARAM_F + ref.NPARAM_I - 1) or \
+        C.sizeof(_lib.NmpParams) == 4 * (ref.NPARAM_F + ref.NPARAM_I)
+
+
+def test_abi_version_and_errors(engine_lib):
+    assert engine_lib.nmp_abi_version() == 1
+    for code in (0, -1, -2, -3, -4, -5, -99):
+        assert engine_lib.nmp_strerror(code)
+    p = _lib.NmpParams()
+    h = C.c_void_p()
+    good = _lib.NmpOptions(*L.options_tuple(L.CASE_NML_OPTIONS))
+    # validation happens before any device is touched
+    bad = _lib.NmpOptions(*L.options_tuple(L.CASE_NML_OPTIONS))
+    bad.opt_run = 5
+    assert engine_lib.nmp_init(C.byref(p), C.byref(bad), 0, 4, C.byref(h)) == -3
+    assert engine_lib.nmp_init(C.byref(p), C.byref(good), 0, 2, C.byref(h)) == -5
+    assert engine_lib.nmp_init(None, C.byref(good), 0, 4, C.byref(h)) == -1
+    with pytest.raises(_lib.NmpError, match="option"):
+        _lib.check(-3, "nmp_init")
+    zs = (C.c_float * 4)(-0.1, -0.4, -1.0, -2.0)
+    assert engine_lib.nmp_step(None, 1, 1, zs, 900.0, 1.0, 366, None, None, None, None, None,
+                               None, 0, None, None) == -1
+
+
+def test_state_from_aos(engine_lib):
+    """168-B noahmp_state_t records -> SoA state (SURVEY 8b mapping table)."""
+    n = 3
+    rec = np.zeros((n, 42), np.float32)
+    ints = rec.view(np.int32)
+    rec[:, 3:7] = [-0.1, -0.4, -1.0, -2.0]             # zsoil
+    rec[:, 10] = [0, 1, 2]                             # nsnow (real, +)
+    ints[:, 11] = [7, 10, 2]                           # lutyp
+    ints[:, 12] = [6, 3, 9]                            # sltyp
+    rec[:, 13], rec[:, 14] = 2.0, 0.5                  # lai, sai
+    rec[:, 16:19] = [280.0, 0.1, 0.0]                  # cantmp, canwat, cansno
+    rec[1, 7:10] = [0.0, 0.0, 0.05]                    # one layer: top at +0.05
+    rec[2, 7:10] = [0.0, 0.30, 0.12]                   # two layers: tops +0.30, +0.12
+    rec[:, 19:22] = 270.0
+    rec[:, 22:25] = 1.0
+    rec[:, 25:28] = 10.0
+    rec[:, 28:32] = [285, 284, 283, 282]
+    rec[:, 32:36] = 0.2
+    rec[:, 36:40] = 0.05
+    rec[:, 40] = 4900.0
+    rec[:, 41] = -2.5                                  # zwt, +up
+    st = np.full((L.NSTATE, n), -1.0, np.float32)
+    isn = np.zeros(n, np.int32)
+    si = np.zeros((L.NSTATIC_I, n), np.int32)
+    assert engine_lib.nmp_state_from_aos(rec.ctypes.data, n, n, st.ctypes.data, isn.ctypes.data,
+                                         si.ctypes.data) == 0
+    assert list(isn) == [0, -1, -2]
+    assert list(si[0]) == [7, 10, 2] and list(si[1]) == [6, 3, 9]
+    np.testing.assert_allclose(st[L.s("SMC")], 0.25)
+    np.testing.assert_allclose(st[L.si("ZWT")], 2.5)
+    np.testing.assert_allclose(st[L.si("WA")], 4900.0)
+    np.testing.assert_allclose(st[L.si("TV")], 280.0)
+    z = st[L.s("ZSNSO")]
+    np.testing.assert_allclose(z[3:, 0], [-0.1, -0.4, -1.0, -2.0])
+    np.testing.assert_allclose(z[2:, 1], [-0.05, -0.15, -0.45, -1.05, -2.05], rtol=1e-6)
+    np.testing.assert_allclose(z[1:, 2], [-0.18, -0.30, -0.40, -0.70, -1.30, -2.30], rtol=1e-6)
+    assert st[L.si("SNOWH"), 2] == pytest.approx(0.30)
+    assert engine_lib.nmp_state_from_aos(rec.ctypes.data, n, n - 1, st.ctypes.data,
+                                         isn.ctypes.data, None) == -1
+
+
+def test_timeman():
+    assert timeman.yearlen(2000) == 366 and timeman.yearlen(1900) == 365
+    assert timeman.yearlen(2001) == 365
+    lat = np.radians([40.0])
+    c_noon = timeman.cosz(lat, np.array([0.0]), 172.5, 366)
+    c_night = timeman.cosz(lat, np.array([0.0]), 172.0, 366)
+    assert c_noon[0] > 0.9 and c_night[0] < 0
+
+
+@pytest.mark.parametrize("kind", ["casenml", "mixed", "conus"])
+def test_case_generator_consistency(ref_params, kind):
+    cols = cases.make_columns(512 if kind != "casenml" else 4, kind, ref_params, seed=3)
+    isn = cols.isnow
+    assert ((isn >= -3) & (isn <= 0)).all()
+    snl = cols.state[L.s("SNICE")]
+    for k in range(3):
+        act = (k - 2) >= isn + 1
+        assert (snl[k, act] > 0).all() and (snl[k, ~act] == 0).all()
+    z = cols.state[L.s("ZSNSO")]
+    assert (np.diff(z, axis=0)[np.isfinite(np.diff(z, axis=0))] <= 0).sum() > 0
+    smc = cols.state[L.s("SMC")]
+    sh2o = cols.state[L.s("SH2O")]
+    assert (sh2o <= smc + 1e-7).all()
+    f = cases.forcing_step(cols, 180.0, 366, 0, seed=1)
+    assert f.shape == (L.NFORCING, cols.n) and np.isfinite(f).all()
