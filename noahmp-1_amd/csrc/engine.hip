@@ -158,8 +158,9 @@ int nmp_step(nmp_engine* eng, int64_t ncol, int64_t ld, const float zsoil[4], fl
              float julian, int32_t yearlen, void* state, int32_t* isnow, const void* static_f,
              const int32_t* static_i, const void* forcing, void* diag, int diag_level,
              int32_t* col_status, void* stream) {
-  if (!eng || !zsoil || ncol < 0 || ld < ncol || !state || !isnow || !static_f || !static_i ||
-      !forcing || !col_status)
+  if (!eng || ncol < 0) return NMP_E_ARG;
+  if (ncol == 0) return NMP_OK;
+  if (!zsoil || ld < ncol || !state || !isnow || !static_f || !static_i || !forcing || !col_status)
     return NMP_E_ARG;
   if (diag_level < NMP_DIAG_NONE || diag_level > NMP_DIAG_FULL) return NMP_E_ARG;
   if (diag_level != NMP_DIAG_NONE && !diag) return NMP_E_ARG;

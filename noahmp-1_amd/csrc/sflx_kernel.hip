@@ -569,7 +569,7 @@ DEV void combine(Col<T>& c, T& ponding1, T& ponding2) {
       if (j > c.isnow + 3 && c.isnow < -1) {
 #pragma unroll
         for (int i = 2; i >= 1; --i) {
-          if (i <= j && i >= c.isnow + 5) {
+          if (i <= j && i >= c.isnow + 4) {  // Fortran I = J .. ISNOW+2
             c.stc[i] = c.stc[i - 1];
             c.snliq[i] = c.snliq[i - 1];
             c.snice[i] = c.snice[i - 1];
@@ -627,7 +627,7 @@ DEV void combine(Col<T>& c, T& ponding1, T& ponding2) {
                   c.stc[i]);
 #pragma unroll
             for (int k = 2; k >= 1; --k) {
-              if (k <= jj - 1 && k >= c.isnow + 5) {
+              if (k <= jj - 1 && k >= c.isnow + 4) {  // Fortran K = J-1 .. ISNOW+2
                 c.stc[k] = c.stc[k - 1];
                 c.snice[k] = c.snice[k - 1];
                 c.snliq[k] = c.snliq[k - 1];
@@ -640,7 +640,7 @@ DEV void combine(Col<T>& c, T& ponding1, T& ponding2) {
                   c.stc[ll]);
 #pragma unroll
             for (int k = 2; k >= 1; --k) {
-              if (k <= i - 1 && k >= c.isnow + 5) {
+              if (k <= i - 1 && k >= c.isnow + 4) {
                 c.stc[k] = c.stc[k - 1];
                 c.snice[k] = c.snice[k - 1];
                 c.snliq[k] = c.snliq[k - 1];

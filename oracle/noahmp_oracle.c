@@ -39,6 +39,36 @@ typedef ORACLE_REAL real;
 #define FMOD fmod
 #define EXP2 exp2
 #define COPYSIGN copysign
+#elif defined(ORACLE_CRMATH)
+/* fp32 arithmetic with correctly rounded elementary functions (evaluated in
+ * double, rounded once) instead of glibc's float libm.  Isolates libm
+ * rounding from the algorithm: the GPU engine's default math mode computes
+ * exactly this, so GPU-vs-CR differences mean a kernel bug, while CR-vs-
+ * reference differences are glibc float-libm ulps (tanhf/atanf chiefly). */
+static inline float cr_exp(float x) { return (float)exp((double)x); }
+static inline float cr_log(float x) { return (float)log((double)x); }
+static inline float cr_log10(float x) { return (float)log10((double)x); }
+static inline float cr_pow(float x, float y) { return (float)pow((double)x, (double)y); }
+static inline float cr_tanh(float x) { return (float)tanh((double)x); }
+static inline float cr_atan(float x) { return (float)atan((double)x); }
+static inline float cr_tan(float x) { return (float)tan((double)x); }
+static inline float cr_acos(float x) { return (float)acos((double)x); }
+static inline float cr_cos(float x) { return (float)cos((double)x); }
+static inline float cr_exp2(float x) { return (float)exp2((double)x); }
+#define EXP cr_exp
+#define LOG cr_log
+#define LOG10 cr_log10
+#define POW cr_pow
+#define SQRT sqrtf
+#define TANH cr_tanh
+#define ATAN cr_atan
+#define TAN cr_tan
+#define ACOS cr_acos
+#define COS cr_cos
+#define FABS fabsf
+#define FMOD fmodf
+#define EXP2 cr_exp2
+#define COPYSIGN copysignf
 #else
 #define EXP expf
 #define LOG logf

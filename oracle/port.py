@@ -15,7 +15,8 @@ from ref import PARAM_FLOAT_FIELDS, PARAM_INT_FIELDS, PARAM_SHAPES, NPARAM_F, NP
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIBS = {4: os.path.join(HERE, "build", "liboracle_f32.so"),
-        8: os.path.join(HERE, "build", "liboracle_f64.so")}
+        8: os.path.join(HERE, "build", "liboracle_f64.so"),
+        "cr": os.path.join(HERE, "build", "liboracle_f32cr.so")}
 NST, NSF, NSI, NFC, NDG = 56, 6, 6, 12, 58
 _libs = {}
 
@@ -44,22 +45,25 @@ def _lib(precision):
         if not available(precision):
             raise FileNotFoundError(f"{LIBS[precision]} missing (run make -C oracle port)")
         lib = C.CDLL(LIBS[precision])
-        rt = np.float32 if precision == 4 else np.float64
+        rt = np.float64 if precision == 8 else np.float32
         rp = np.ctypeslib.ndpointer(rt, flags="C_CONTIGUOUS")
         ip = np.ctypeslib.ndpointer(np.int32, flags="C_CONTIGUOUS")
-        creal = C.c_float if precision == 4 else C.c_double
+        creal = C.c_double if precision == 8 else C.c_float
         lib.oracle_sflx_batch.argtypes = [C.c_int32, creal, C.c_int32, creal, rp, rp, ip, rp, ip,
                                           rp, rp, ip, C.c_char_p, C.c_void_p]
         lib.oracle_sflx_run.argtypes = [C.c_int32, C.c_int32, creal, C.c_int32, creal, rp, rp, ip,
                                         rp, ip, rp, C.c_int32, rp, ip, C.c_char_p, C.c_void_p]
-        assert lib.oracle_real_bytes() == precision
+        assert lib.oracle_real_bytes() == (4 if precision == "cr" else precision)
         _libs[precision] = (lib, rt)
     return _libs[precision]
 
 
 def step(P: dict, options, zsoil, dt, yearlen, julian, state, isnow, static_f, static_i, forcing,
-         precision: int = 4):
-    """One step of the C restatement.  SoA in, SoA out: (state', isnow', diag(58,n), status)."""
+         precision=4):
+    """One step of the C restatement.  SoA in, SoA out: (state', isnow', diag(58,n), status).
+
+    precision: 4 (bit-exact to the reference), 8 (fp64), or "cr" (fp32 with
+    correctly rounded libm -- what the engine's default math computes)."""
     lib, rt = _lib(precision)
     n = isnow.shape[0]
     st = np.ascontiguousarray(np.asarray(state, rt).T)

@@ -32,8 +32,9 @@ def bit_equal(a, b) -> np.ndarray:
 def close(got, exp, rtol, atol) -> np.ndarray:
     got = np.asarray(got, np.float64)
     exp = np.asarray(exp, np.float64)
-    both_nan = np.isnan(got) & np.isnan(exp)
-    return both_nan | (np.abs(got - exp) <= atol + rtol * np.abs(exp))
+    same = (got == exp) | (np.isnan(got) & np.isnan(exp))
+    with np.errstate(invalid="ignore", over="ignore"):
+        return same | (np.abs(got - exp) <= atol + rtol * np.abs(exp))
 
 
 def column_mismatch(got, exp, rtol, atol, names=None):
@@ -60,3 +61,44 @@ def as_ref_status(status) -> np.ndarray:
     hit = (s & (4 | 16)) != 0
     s[hit] = (s[hit] & ~(4 | 16)) | 128
     return s
+
+
+# Parity bar against the reference fixtures (SURVEY.md 8c tolerances).  A
+# one-ulp libm difference can change a Newton iteration count or a limiter
+# branch (H12), so the bar is per column: TOL_FRAC of the columns must be
+# inside the tight tolerance and every column inside the loose envelope,
+# except for columns where the reference itself sits on a threshold tie (ISNOW
+# or a fatal-status flip), which are counted separately.
+STATE_TOL = (1e-5, 1e-4)    # rel, abs (K, m, mm, m3/m3 ...)
+DIAG_TOL = (1e-4, 1e-2)     # rel, abs (W/m2, mm/s ...)
+STATE_LOOSE = (1e-3, 1e-3)
+DIAG_LOOSE = (2e-2, 1.0)
+TOL_FRAC = 0.97     # columns inside the tight tolerance
+LOOSE_FRAC = 0.995  # non-tie columns inside the loose envelope
+TIE_FRAC = 0.02     # columns with an ISNOW or fatal-status flip
+
+
+def parity_vs_reference(st, isn, dg, status, g, state_key="state1", diag_key="diag",
+                        isnow_key="isnow1", status_key="status", tol_frac=TOL_FRAC,
+                        loose_frac=LOOSE_FRAC, tie_frac=TIE_FRAC):
+    """Returns a dict of per-column fractions and a failure message (or '')."""
+    est, edg = g[state_key], g[diag_key]
+    tie = (isn != g[isnow_key]) | (as_ref_status(status) != g[status_key])
+    tight = close(st, est, *STATE_TOL).all(0) & close(dg, edg, *DIAG_TOL).all(0)
+    loose = close(st, est, *STATE_LOOSE).all(0) & close(dg, edg, *DIAG_LOOSE).all(0)
+    exact = (bit_equal(st, est).all(0) & bit_equal(dg, edg).all(0))
+    r = dict(n=int(isn.size), exact=float(exact.mean()), tight=float(tight.mean()),
+             loose_nontie=float(loose[~tie].mean()) if (~tie).any() else 1.0,
+             tie=float(tie.mean()))
+    msg = []
+    if r["tight"] < tol_frac and (~tight).sum() > 1:
+        msg.append(f"only {r['tight']:.3f} of columns within the tight tolerance")
+    if r["loose_nontie"] < loose_frac and (~loose & ~tie).sum() > 1:
+        msg.append(f"{int((~loose & ~tie).sum())} non-tie columns outside the loose envelope")
+    if r["tie"] > tie_frac and tie.sum() > 1:
+        msg.append(f"{int(tie.sum())} columns with ISNOW/status flips")
+    if msg:
+        _, rep_s = column_mismatch(st[:, ~tie], est[:, ~tie], *STATE_LOOSE)
+        _, rep_d = column_mismatch(dg[:, ~tie], edg[:, ~tie], *DIAG_LOOSE)
+        msg.append("loose-envelope misses: " + "; ".join(rep_s[:6] + rep_d[:6]))
+    return r, " | ".join(msg)

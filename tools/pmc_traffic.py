@@ -1,0 +1,82 @@
+"""Turn rocprofv3 PMC CSVs (tools/pmc_run.sh) into profiles/traffic.json.
+
+HBM bytes per engine launch = FETCH_SIZE * read-correction + WRITE_SIZE *
+write-correction, where the corrections come from the calibration copy
+(tools/calib_copy.hip: same SoA 4 B/lane pattern, known byte counts), per
+/opt/skills/guides/MI355X_MICROARCH.md (HBM section: FETCH_SIZE is
+uncalibrated for non-16B accesses; calibrate on your own pattern).
+FETCH_SIZE/WRITE_SIZE are reported in KB (1024 B) by rocprofv3.
+
+usage: python tools/pmc_traffic.py gpurun_out/<tag> [--ncol N]
+"""
+import csv
+import glob
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+KERNEL = "sflx_step_kernel"
+
+
+def counters(d, counter):
+    """{dispatch_id: (kernel_name, value)} from a counter_collection.csv under d."""
+    files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
+    assert files, f"no counter_collection.csv under {d}"
+    out = {}
+    for fn in files:
+        with open(fn) as f:
+            for row in csv.DictReader(f):
+                r = {k.lower(): v for k, v in row.items()}
+                if r.get("counter_name") != counter:
+                    continue
+                did = r.get("dispatch_id") or r.get("correlation_id")
+                name = r.get("kernel_name", "")
+                v = float(r["counter_value"])
+                k0 = out.get(did, (name, 0.0))
+                out[did] = (name, k0[1] + v)  # sum over dimension instances
+    return out
+
+
+def mean_for(d, counter, pat):
+    vals = [v for (n, v) in counters(d, counter).values() if pat in n]
+    assert vals, (d, counter, pat)
+    return sum(vals) / len(vals), len(vals)
+
+
+def main():
+    base = sys.argv[1]
+    ncol = 1 << 20
+    if "--ncol" in sys.argv:
+        ncol = int(sys.argv[sys.argv.index("--ncol") + 1])
+    calib_n, nf = 4194304, 56
+    cal_bytes = nf * calib_n * 4
+    cf, _ = mean_for(os.path.join(base, "calib_FETCH_SIZE"), "FETCH_SIZE", "calib_soa_copy")
+    cw, _ = mean_for(os.path.join(base, "calib_WRITE_SIZE"), "WRITE_SIZE", "calib_soa_copy")
+    rf = cal_bytes / (cf * 1024.0)
+    rw = cal_bytes / (cw * 1024.0)
+    bf, nb = mean_for(os.path.join(base, "bench_FETCH_SIZE"), "FETCH_SIZE", KERNEL)
+    bw, _ = mean_for(os.path.join(base, "bench_WRITE_SIZE"), "WRITE_SIZE", KERNEL)
+    rd = bf * 1024.0 * rf
+    wr = bw * 1024.0 * rw
+    res = {"ncol": ncol, "precision": 4, "math": "ref", "kernel": KERNEL, "dispatches": nb,
+           "fetch_size_kb": bf, "write_size_kb": bw, "read_correction": rf,
+           "write_correction": rw, "read_bytes": rd, "write_bytes": wr,
+           "bytes_per_launch": rd + wr, "bytes_per_colstep": (rd + wr) / ncol,
+           "source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes ({base})"}
+    sq = os.path.join(base, "bench_SQ")
+    if os.path.isdir(sq):
+        for c in ("SQ_INSTS_VALU", "SQ_WAVES", "SQ_INSTS_SALU", "SQ_INSTS_VMEM_RD",
+                  "SQ_INSTS_VMEM_WR"):
+            try:
+                res[c] = mean_for(sq, c, KERNEL)[0]
+            except AssertionError:
+                pass
+    out = os.path.join(ROOT, "profiles", "traffic.json")
+    with open(out, "w") as f:
+        json.dump(res, f, indent=1)
+    print(json.dumps(res, indent=1))
+
+
+if __name__ == "__main__":
+    main()
