@@ -172,8 +172,10 @@ def main():
         if os.path.exists(a.traffic):
             with open(a.traffic) as f:
                 tj = json.load(f)
+            from noahmp_amd import build as _build
             if tj.get("ncol") == n and tj.get("precision") == a.precision and \
-                    tj.get("math") == a.math:
+                    tj.get("math") == a.math and tj.get("source_hash") == _build.source_hash() \
+                    and os.environ.get("NOAHMP_ENGINE_LIB") is None:
                 traffic = tj.get("bytes_per_launch")
         line = {
             "metric": METRIC, "value": value, "unit": "column-steps/s", "n_gpus": world,

@@ -14,13 +14,26 @@ PKG = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(PKG)
 CSRC = os.path.join(PKG, "csrc")
 LIB_DIR = os.path.join(PKG, "lib")
-LIB_PATH = os.path.join(LIB_DIR, "libnoahmp_engine.so")
+LIB_PATH = os.environ.get("NOAHMP_ENGINE_LIB") or os.path.join(LIB_DIR, "libnoahmp_engine.so")
 SOURCES = ["engine.hip", "sflx_kernel.hip", "tables.cpp"]
 HEADERS = ["dev_params.h", "sflx_kargs.h", "sflx_math.h"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")
 FLAGS = ["-O3", f"--offload-arch={ARCH}", "-fPIC", "-shared", "-std=c++17",
          "-ffp-contract=off", "-Wno-unused-result", "-Wno-unused-value"]
+
+
+def source_hash() -> str:
+    """Hash of every engine source + build flag: identifies the kernel a
+    measurement (profiles/traffic.json) was taken on."""
+    import hashlib
+    h = hashlib.sha256(" ".join(FLAGS).encode())
+    for p in sorted(SOURCES + HEADERS):
+        with open(os.path.join(CSRC, p), "rb") as f:
+            h.update(f.read())
+    with open(os.path.join(ROOT, "include", "noahmp_engine.h"), "rb") as f:
+        h.update(f.read())
+    return h.hexdigest()[:16]
 
 
 def _newest_input() -> float:
@@ -30,18 +43,21 @@ def _newest_input() -> float:
     return max(os.path.getmtime(p) for p in paths)
 
 
-def build(force: bool = False, verbose: bool = True) -> str:
-    if not force and os.path.exists(LIB_PATH) and os.path.getmtime(LIB_PATH) >= _newest_input():
-        return LIB_PATH
-    os.makedirs(LIB_DIR, exist_ok=True)
-    tmp = LIB_PATH + ".tmp"
-    cmd = [HIPCC, *FLAGS, "-I", os.path.join(ROOT, "include"), "-I", CSRC, "-o", tmp,
+def build(force: bool = False, verbose: bool = True, out: str | None = None,
+          extra: tuple = ()) -> str:
+    """Build the engine library (default: LIB_PATH; `out`/`extra` for tuning variants)."""
+    path = out or LIB_PATH
+    if not force and os.path.exists(path) and os.path.getmtime(path) >= _newest_input():
+        return path
+    os.makedirs(os.path.dirname(path), exist_ok=True)
+    tmp = path + ".tmp"
+    cmd = [HIPCC, *FLAGS, *extra, "-I", os.path.join(ROOT, "include"), "-I", CSRC, "-o", tmp,
            *[os.path.join(CSRC, s) for s in SOURCES]]
     if verbose:
         print("[noahmp build]", " ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)
-    os.replace(tmp, LIB_PATH)
-    return LIB_PATH
+    os.replace(tmp, path)
+    return path
 
 
 if __name__ == "__main__":

@@ -743,9 +743,40 @@ DEV void divide(Col<T>& c) {
 
 // ---------------------------------------------------------------------------
 // noahmp_sflx for one column: func.f90:66-476
+// Output sink: diagnostics and final state fields are written to HBM at the
+// point they become final (not held in registers to the end of the step).
+__host__ __device__ constexpr int out_index(int d) {
+  return d == NMP_D_FSA ? NMP_O_FSA : d == NMP_D_FSR ? NMP_O_FSR : d == NMP_D_FIRA ? NMP_O_FIRA
+       : d == NMP_D_FSH ? NMP_O_FSH : d == NMP_D_SSOIL ? NMP_O_SSOIL : d == NMP_D_FCEV ? NMP_O_FCEV
+       : d == NMP_D_FGEV ? NMP_O_FGEV : d == NMP_D_FCTR ? NMP_O_FCTR : d == NMP_D_ECAN ? NMP_O_ECAN
+       : d == NMP_D_ETRAN ? NMP_O_ETRAN : d == NMP_D_EDIR ? NMP_O_EDIR : d == NMP_D_TRAD ? NMP_O_TRAD
+       : d == NMP_D_RUNSRF ? NMP_O_RUNSRF : d == NMP_D_RUNSUB ? NMP_O_RUNSUB
+       : d == NMP_D_ALBEDO ? NMP_O_ALBEDO : -1;
+}
+
+template <class T>
+struct Sink {
+  T* dg;        // diag + column (NULL when level == NMP_DIAG_NONE)
+  T* st;        // state + column
+  int64_t ld;
+  int level;
+  template <int D>
+  DEV void d(T v) const {
+    if (level == NMP_DIAG_FULL) {
+      dg[D * ld] = v;
+    } else if (level == NMP_DIAG_OUT) {
+      constexpr int o = out_index(D);
+      if (o >= 0) dg[o * ld] = v;
+    }
+  }
+  DEV void t2m(T v) const {
+    if (level == NMP_DIAG_OUT) dg[NMP_O_T2M * ld] = v;
+  }
+  DEV void s(int f, T v) const { st[f * ld] = v; }
+};
+
 template <class T, bool R>
-DEV void sflx_column(const DevParams& P, const KArgs<T>& A, Col<T>& c, T (&dout)[NMP_NDIAG_FULL],
-                     T& t2m_out) {
+DEV void sflx_column(const DevParams& P, const KArgs<T>& A, Col<T>& c, const Sink<T>& out) {
   typedef Mth<T, R> M;
   const Opt& o = A.o;
   const VegRec& V = P.veg[c.lutyp - 1];
@@ -1043,6 +1074,16 @@ DEV void sflx_column(const DevParams& P, const KArgs<T>& A, Col<T>& c, T (&dout)
     }
     fsr = (albd[0] * solad + albi[0] * solai) + (albd[1] * solad + albi[1] * solai);
   }
+  if (fabs(swdown - (fsa + fsr)) > L(0.01)) c.status |= NMP_ST_ERRSW;  // error() :688-710
+  out.template d<NMP_D_FSA>(fsa);
+  out.template d<NMP_D_FSR>(fsr);
+  out.template d<NMP_D_ALBEDO>((swdown != L(0.0)) ? fsr / swdown : L(-999.9));  // :470-474
+  out.template d<NMP_D_FSNO>(fsno);
+  out.template d<NMP_D_FVEG>(fveg);
+  out.template d<NMP_D_BGAP>(bgap);
+  out.template d<NMP_D_WGAP>(wgap);
+  out.s(NMP_S_ALBOLD, c.albold);
+  out.s(NMP_S_TAUSS, c.tauss);
   T emv = L(1.0) - M::exp(-(elai + esai) / L(1.0));
   T emg;
   if (c.ice == 1)
@@ -1361,6 +1402,49 @@ DEV void sflx_column(const DevParams& P, const KArgs<T>& A, Col<T>& c, T (&dout)
   T trad = M::pow((fire - (L(1.0) - emissi) * c.lwdn) / (emissi * SB), L(0.25));
   T apar = parsun * laisun + parsha * laisha;
   T psn = psnsun * laisun + psnsha * laisha;
+  // error(): energy balance (func.f90:712-721), a function of final energy terms only
+  if (fabs(sav + sag - (fira + fsh + fcev + fgev + fctr + ssoil)) > L(0.01))
+    c.status |= NMP_ST_ERRENG;
+  out.template d<NMP_D_SAV>(sav);
+  out.template d<NMP_D_SAG>(sag);
+  out.template d<NMP_D_FIRA>(fira);
+  out.template d<NMP_D_SSOIL>(ssoil);
+  out.template d<NMP_D_FSH>(fsh);
+  out.template d<NMP_D_FCEV>(fcev);
+  out.template d<NMP_D_FGEV>(fgev);
+  out.template d<NMP_D_FCTR>(fctr);
+  out.template d<NMP_D_TRAD>(trad);
+  out.template d<NMP_D_T2MV>(t2mv);
+  out.template d<NMP_D_T2MB>(t2mb);
+  out.template d<NMP_D_Q2V>(q2v);
+  out.template d<NMP_D_APAR>(apar);
+  out.template d<NMP_D_PSN>(psn);
+  out.template d<NMP_D_RSSUN>(rssun);
+  out.template d<NMP_D_RSSHA>(rssha);
+  out.template d<NMP_D_CHV>(chv);
+  out.template d<NMP_D_CHB>(chb);
+  out.template d<NMP_D_EMISSI>(emissi);
+  out.template d<NMP_D_SHG>(shg);
+  out.template d<NMP_D_SHC>(shc);
+  out.template d<NMP_D_SHB>(shb);
+  out.template d<NMP_D_EVG>(evg);
+  out.template d<NMP_D_EVB>(evb);
+  out.template d<NMP_D_GHV>(ghv);
+  out.template d<NMP_D_GHB>(ghb);
+  out.template d<NMP_D_IRG>(irg);
+  out.template d<NMP_D_IRC>(irc);
+  out.template d<NMP_D_IRB>(irb);
+  out.template d<NMP_D_TR>(tr);
+  out.template d<NMP_D_EVC>(evc);
+  out.template d<NMP_D_CHLEAF>(chleaf);
+  out.template d<NMP_D_CHUC>(chuc);
+  out.template d<NMP_D_CHV2>(chv2);
+  out.template d<NMP_D_CHB2>(chb2);
+  out.t2m(t2m);
+  out.s(NMP_S_TAH, c.tah);
+  out.s(NMP_S_EAH, c.eah);
+  out.s(NMP_S_CM, c.cm);
+  out.s(NMP_S_CH, c.ch);
 
   // tsnosoi + hrt + hstep (func.f90:3987-4237), layers kt..6 in VGPRs
   {
@@ -1439,6 +1523,9 @@ DEV void sflx_column(const DevParams& P, const KArgs<T>& A, Col<T>& c, T (&dout)
       c.tg = (veg && fveg > L(0.0)) ? fveg * tgv + (L(1.0) - fveg) * tgb : tgb;
     }
   }
+  out.template d<NMP_D_TGB>(tgb);
+  out.template d<NMP_D_TGV>(tgv);
+  out.s(NMP_S_TG, c.tg);
 
   // phasechange: func.f90:4291-4491
   T qmelt = L(0.0), ponding = L(0.0);
@@ -1596,6 +1683,7 @@ DEV void sflx_column(const DevParams& P, const KArgs<T>& A, Col<T>& c, T (&dout)
     (void)xmf;
   }
   // ===================== end energy =====================
+  out.template d<NMP_D_PONDING>(ponding);
 
 #pragma unroll
   for (int k = 0; k < 4; ++k) c.sice[k] = rmax(L(0.0), c.smc[k] - c.sh2o[k]);
@@ -1603,6 +1691,8 @@ DEV void sflx_column(const DevParams& P, const KArgs<T>& A, Col<T>& c, T (&dout)
   const T qvap = rmax(fgev / latheag, L(0.0));
   const T qdew = fabs(rmin(fgev / latheag, L(0.0)));
   const T edir = qvap - qdew;
+  out.template d<NMP_D_EDIR>(edir);
+  out.s(NMP_S_SNEQVO, c.sneqvo);
 
   // ===================== water: func.f90:4601-4804 =====================
   T ecan, etran, runsrf = L(0.0), runsub = L(0.0), qsnbot = L(0.0), ponding1 = L(0.0);
@@ -1698,6 +1788,9 @@ DEV void sflx_column(const DevParams& P, const KArgs<T>& A, Col<T>& c, T (&dout)
       snowhin = L(0.0);
     }
   }
+  out.template d<NMP_D_ECAN>(ecan);
+  out.template d<NMP_D_ETRAN>(etran);
+  out.template d<NMP_D_FPICE>(fpice);
   T qsnsub = (c.sneqv > L(0.0)) ? rmin(qvap, c.sneqv / DT) : L(0.0);
   T qseva = qvap - qsnsub;
   T qsnfro = (c.sneqv > L(0.0)) ? qdew : L(0.0);
@@ -2258,6 +2351,11 @@ DEV void sflx_column(const DevParams& P, const KArgs<T>& A, Col<T>& c, T (&dout)
   }
   runsub = runsub + snoflow;
   // ===================== end water =====================
+  out.template d<NMP_D_RUNSRF>(runsrf);
+  out.template d<NMP_D_RUNSUB>(runsub);
+  out.template d<NMP_D_QSNBOT>(qsnbot);
+  out.template d<NMP_D_PONDING1>(ponding1);
+  out.template d<NMP_D_PONDING2>(ponding2);
 
   // carbon + co2flux (opt_veg 2|5): func.f90:6642-7025
   T gpp = L(0.0), npp = L(0.0), nee = L(0.0);
@@ -2348,10 +2446,9 @@ DEV void sflx_column(const DevParams& P, const KArgs<T>& A, Col<T>& c, T (&dout)
     }
   }
 
-  // error(): energy / shortwave balance checks (func.f90:633-732)
-  if (fabs(swdown - (fsa + fsr)) > L(0.01)) c.status |= NMP_ST_ERRSW;
-  if (fabs(sav + sag - (fira + fsh + fcev + fgev + fctr + ssoil)) > L(0.01))
-    c.status |= NMP_ST_ERRENG;
+  out.template d<NMP_D_NEE>(nee);
+  out.template d<NMP_D_GPP>(gpp);
+  out.template d<NMP_D_NPP>(npp);
   // urban QSFC (:459-463)
   if (c.lutyp == P.g.isurban) {
     T qfx = etran + ecan + edir;
@@ -2362,31 +2459,19 @@ DEV void sflx_column(const DevParams& P, const KArgs<T>& A, Col<T>& c, T (&dout)
     c.snowh = L(0.0);
     c.sneqv = L(0.0);
   }
-  T albedo = (swdown != L(0.0)) ? fsr / swdown : L(-999.9);
-
-  dout[NMP_D_FSA] = fsa; dout[NMP_D_FSR] = fsr; dout[NMP_D_FIRA] = fira; dout[NMP_D_FSH] = fsh;
-  dout[NMP_D_SSOIL] = ssoil; dout[NMP_D_FCEV] = fcev; dout[NMP_D_FGEV] = fgev;
-  dout[NMP_D_FCTR] = fctr; dout[NMP_D_ECAN] = ecan; dout[NMP_D_ETRAN] = etran;
-  dout[NMP_D_EDIR] = edir; dout[NMP_D_TRAD] = trad; dout[NMP_D_TGB] = tgb; dout[NMP_D_TGV] = tgv;
-  dout[NMP_D_T2MV] = t2mv; dout[NMP_D_T2MB] = t2mb; dout[NMP_D_Q2V] = q2v; dout[NMP_D_Q2B] = q2b;
-  dout[NMP_D_RUNSRF] = runsrf; dout[NMP_D_RUNSUB] = runsub; dout[NMP_D_APAR] = apar;
-  dout[NMP_D_PSN] = psn; dout[NMP_D_SAV] = sav; dout[NMP_D_SAG] = sag; dout[NMP_D_FSNO] = fsno;
-  dout[NMP_D_NEE] = nee; dout[NMP_D_GPP] = gpp; dout[NMP_D_NPP] = npp; dout[NMP_D_FVEG] = fveg;
-  dout[NMP_D_ALBEDO] = albedo; dout[NMP_D_QSNBOT] = qsnbot; dout[NMP_D_PONDING] = ponding;
-  dout[NMP_D_PONDING1] = ponding1; dout[NMP_D_PONDING2] = ponding2; dout[NMP_D_RSSUN] = rssun;
-  dout[NMP_D_RSSHA] = rssha; dout[NMP_D_BGAP] = bgap; dout[NMP_D_WGAP] = wgap;
-  dout[NMP_D_CHV] = chv; dout[NMP_D_CHB] = chb; dout[NMP_D_EMISSI] = emissi;
-  dout[NMP_D_SHG] = shg; dout[NMP_D_SHC] = shc; dout[NMP_D_SHB] = shb; dout[NMP_D_EVG] = evg;
-  dout[NMP_D_EVB] = evb; dout[NMP_D_GHV] = ghv; dout[NMP_D_GHB] = ghb; dout[NMP_D_IRG] = irg;
-  dout[NMP_D_IRC] = irc; dout[NMP_D_IRB] = irb; dout[NMP_D_TR] = tr; dout[NMP_D_EVC] = evc;
-  dout[NMP_D_CHLEAF] = chleaf; dout[NMP_D_CHUC] = chuc; dout[NMP_D_CHV2] = chv2;
-  dout[NMP_D_CHB2] = chb2; dout[NMP_D_FPICE] = fpice;
-  t2m_out = t2m;
+  out.template d<NMP_D_Q2B>(q2b);
 }
 
 // ---------------------------------------------------------------------------
 template <class T, bool R>
-__global__ __launch_bounds__(256) void sflx_step_kernel(const DevParams* __restrict__ gparams,
+// Occupancy target: 2 waves/SIMD for fp32 (256 VGPRs; measured faster than
+// 1 wave with 500 VGPRs and than 3-4 waves with heavy spilling), 1 for fp64.
+#ifndef NMP_WAVES_PER_EU
+#define NMP_WAVES_PER_EU 2
+#endif
+__global__ __launch_bounds__(256)
+__attribute__((amdgpu_waves_per_eu(sizeof(T) == 4 ? NMP_WAVES_PER_EU : 1)))
+void sflx_step_kernel(const DevParams* __restrict__ gparams,
                                                           KArgs<T> a) {
   __shared__ __attribute__((aligned(16))) DevParams sp;
   {
@@ -2441,9 +2526,8 @@ __global__ __launch_bounds__(256) void sflx_step_kernel(const DevParams* __restr
   c.cosz = fc[NMP_A_COSZ * ld]; c.co2air = fc[NMP_A_CO2AIR * ld]; c.o2air = fc[NMP_A_O2AIR * ld];
   c.status = 0;
 
-  T d[NMP_NDIAG_FULL];
-  T t2m;
-  sflx_column<T, R>(sp, a, c, d, t2m);
+  const Sink<T> out{a.diag ? a.diag + c0 : nullptr, a.state + c0, ld, a.diag_level};
+  sflx_column<T, R>(sp, a, c, out);
 
   T* so = a.state + c0;
 #pragma unroll
@@ -2461,33 +2545,17 @@ __global__ __launch_bounds__(256) void sflx_step_kernel(const DevParams* __restr
     so[(NMP_S_SH2O + k) * ld] = c.sh2o[k];
     so[(NMP_S_SMC + k) * ld] = c.smc[k];
   }
-  so[NMP_S_TV * ld] = c.tv; so[NMP_S_TG * ld] = c.tg; so[NMP_S_TAH * ld] = c.tah;
-  so[NMP_S_EAH * ld] = c.eah; so[NMP_S_FWET * ld] = c.fwet; so[NMP_S_CANLIQ * ld] = c.canliq;
+  so[NMP_S_TV * ld] = c.tv;
+  so[NMP_S_FWET * ld] = c.fwet; so[NMP_S_CANLIQ * ld] = c.canliq;
   so[NMP_S_CANICE * ld] = c.canice; so[NMP_S_QSFC * ld] = c.qsfc; so[NMP_S_SNOWH * ld] = c.snowh;
-  so[NMP_S_SNEQV * ld] = c.sneqv; so[NMP_S_SNEQVO * ld] = c.sneqvo;
-  so[NMP_S_ALBOLD * ld] = c.albold; so[NMP_S_TAUSS * ld] = c.tauss;
+  so[NMP_S_SNEQV * ld] = c.sneqv;
   so[NMP_S_QSNOW * ld] = c.qsnow; so[NMP_S_ZWT * ld] = c.zwt; so[NMP_S_WA * ld] = c.wa;
   so[NMP_S_WT * ld] = c.wt; so[NMP_S_WSLAKE * ld] = c.wslake; so[NMP_S_LAI * ld] = c.lai;
   so[NMP_S_SAI * ld] = c.sai; so[NMP_S_LFMASS * ld] = c.lfmass; so[NMP_S_RTMASS * ld] = c.rtmass;
   so[NMP_S_STMASS * ld] = c.stmass; so[NMP_S_WOOD * ld] = c.wood; so[NMP_S_STBLCP * ld] = c.stblcp;
-  so[NMP_S_FASTCP * ld] = c.fastcp; so[NMP_S_CM * ld] = c.cm; so[NMP_S_CH * ld] = c.ch;
+  so[NMP_S_FASTCP * ld] = c.fastcp;
   a.isnow[c0] = c.isnow;
   if (c.status != 0) a.status[c0] |= c.status;
-  if (a.diag_level == NMP_DIAG_FULL) {
-    T* dg = a.diag + c0;
-#pragma unroll
-    for (int k = 0; k < NMP_NDIAG_FULL; ++k) dg[k * ld] = d[k];
-  } else if (a.diag_level == NMP_DIAG_OUT) {
-    T* dg = a.diag + c0;
-    dg[NMP_O_FSA * ld] = d[NMP_D_FSA]; dg[NMP_O_FSR * ld] = d[NMP_D_FSR];
-    dg[NMP_O_FIRA * ld] = d[NMP_D_FIRA]; dg[NMP_O_FSH * ld] = d[NMP_D_FSH];
-    dg[NMP_O_SSOIL * ld] = d[NMP_D_SSOIL]; dg[NMP_O_FCEV * ld] = d[NMP_D_FCEV];
-    dg[NMP_O_FGEV * ld] = d[NMP_D_FGEV]; dg[NMP_O_FCTR * ld] = d[NMP_D_FCTR];
-    dg[NMP_O_ECAN * ld] = d[NMP_D_ECAN]; dg[NMP_O_ETRAN * ld] = d[NMP_D_ETRAN];
-    dg[NMP_O_EDIR * ld] = d[NMP_D_EDIR]; dg[NMP_O_TRAD * ld] = d[NMP_D_TRAD];
-    dg[NMP_O_RUNSRF * ld] = d[NMP_D_RUNSRF]; dg[NMP_O_RUNSUB * ld] = d[NMP_D_RUNSUB];
-    dg[NMP_O_T2M * ld] = t2m; dg[NMP_O_ALBEDO * ld] = d[NMP_D_ALBEDO];
-  }
 }
 
 // launch wrapper (one instantiation per precision / math policy)

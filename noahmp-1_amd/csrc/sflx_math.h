@@ -15,6 +15,14 @@
 #include <hip/hip_runtime.h>
 #include <math.h>
 
+// Math wrappers are inlined by default; -DNMP_MATH_OUTLINE keeps one copy of
+// each (smaller code, fewer instruction-cache misses, call overhead instead).
+#ifdef NMP_MATH_OUTLINE
+#define NMP_MATH_FN static __device__ __noinline__
+#else
+#define NMP_MATH_FN static __device__ __forceinline__
+#endif
+
 namespace nmp {
 
 template <class T, bool REF>
@@ -22,48 +30,48 @@ struct Mth;
 
 template <bool REF>
 struct Mth<double, REF> {
-  static __device__ __forceinline__ double exp(double x) { return ::exp(x); }
-  static __device__ __forceinline__ double exp2(double x) { return ::exp2(x); }
-  static __device__ __forceinline__ double log(double x) { return ::log(x); }
-  static __device__ __forceinline__ double log10(double x) { return ::log10(x); }
-  static __device__ __forceinline__ double pow(double x, double y) { return ::pow(x, y); }
-  static __device__ __forceinline__ double tanh(double x) { return ::tanh(x); }
-  static __device__ __forceinline__ double atan(double x) { return ::atan(x); }
-  static __device__ __forceinline__ double tan(double x) { return ::tan(x); }
-  static __device__ __forceinline__ double acos(double x) { return ::acos(x); }
-  static __device__ __forceinline__ double cos(double x) { return ::cos(x); }
+  NMP_MATH_FN double exp(double x) { return ::exp(x); }
+  NMP_MATH_FN double exp2(double x) { return ::exp2(x); }
+  NMP_MATH_FN double log(double x) { return ::log(x); }
+  NMP_MATH_FN double log10(double x) { return ::log10(x); }
+  NMP_MATH_FN double pow(double x, double y) { return ::pow(x, y); }
+  NMP_MATH_FN double tanh(double x) { return ::tanh(x); }
+  NMP_MATH_FN double atan(double x) { return ::atan(x); }
+  NMP_MATH_FN double tan(double x) { return ::tan(x); }
+  NMP_MATH_FN double acos(double x) { return ::acos(x); }
+  NMP_MATH_FN double cos(double x) { return ::cos(x); }
   static __device__ __forceinline__ double sqrt(double x) { return ::sqrt(x); }
 };
 
 template <>
 struct Mth<float, false> {
-  static __device__ __forceinline__ float exp(float x) { return ::expf(x); }
-  static __device__ __forceinline__ float exp2(float x) { return ::exp2f(x); }
-  static __device__ __forceinline__ float log(float x) { return ::logf(x); }
-  static __device__ __forceinline__ float log10(float x) { return ::log10f(x); }
-  static __device__ __forceinline__ float pow(float x, float y) { return ::powf(x, y); }
-  static __device__ __forceinline__ float tanh(float x) { return ::tanhf(x); }
-  static __device__ __forceinline__ float atan(float x) { return ::atanf(x); }
-  static __device__ __forceinline__ float tan(float x) { return ::tanf(x); }
-  static __device__ __forceinline__ float acos(float x) { return ::acosf(x); }
-  static __device__ __forceinline__ float cos(float x) { return ::cosf(x); }
+  NMP_MATH_FN float exp(float x) { return ::expf(x); }
+  NMP_MATH_FN float exp2(float x) { return ::exp2f(x); }
+  NMP_MATH_FN float log(float x) { return ::logf(x); }
+  NMP_MATH_FN float log10(float x) { return ::log10f(x); }
+  NMP_MATH_FN float pow(float x, float y) { return ::powf(x, y); }
+  NMP_MATH_FN float tanh(float x) { return ::tanhf(x); }
+  NMP_MATH_FN float atan(float x) { return ::atanf(x); }
+  NMP_MATH_FN float tan(float x) { return ::tanf(x); }
+  NMP_MATH_FN float acos(float x) { return ::acosf(x); }
+  NMP_MATH_FN float cos(float x) { return ::cosf(x); }
   static __device__ __forceinline__ float sqrt(float x) { return ::sqrtf(x); }
 };
 
 template <>
 struct Mth<float, true> {
-  static __device__ __forceinline__ float exp(float x) { return (float)::exp((double)x); }
-  static __device__ __forceinline__ float exp2(float x) { return (float)::exp2((double)x); }
-  static __device__ __forceinline__ float log(float x) { return (float)::log((double)x); }
-  static __device__ __forceinline__ float log10(float x) { return (float)::log10((double)x); }
-  static __device__ __forceinline__ float pow(float x, float y) {
+  NMP_MATH_FN float exp(float x) { return (float)::exp((double)x); }
+  NMP_MATH_FN float exp2(float x) { return (float)::exp2((double)x); }
+  NMP_MATH_FN float log(float x) { return (float)::log((double)x); }
+  NMP_MATH_FN float log10(float x) { return (float)::log10((double)x); }
+  NMP_MATH_FN float pow(float x, float y) {
     return (float)::pow((double)x, (double)y);
   }
-  static __device__ __forceinline__ float tanh(float x) { return (float)::tanh((double)x); }
-  static __device__ __forceinline__ float atan(float x) { return (float)::atan((double)x); }
-  static __device__ __forceinline__ float tan(float x) { return (float)::tan((double)x); }
-  static __device__ __forceinline__ float acos(float x) { return (float)::acos((double)x); }
-  static __device__ __forceinline__ float cos(float x) { return (float)::cos((double)x); }
+  NMP_MATH_FN float tanh(float x) { return (float)::tanh((double)x); }
+  NMP_MATH_FN float atan(float x) { return (float)::atan((double)x); }
+  NMP_MATH_FN float tan(float x) { return (float)::tan((double)x); }
+  NMP_MATH_FN float acos(float x) { return (float)::acos((double)x); }
+  NMP_MATH_FN float cos(float x) { return (float)::cos((double)x); }
   static __device__ __forceinline__ float sqrt(float x) { return ::sqrtf(x); }
 };
 
@@ -83,11 +91,19 @@ __device__ __forceinline__ T p5(T x) { return x * p4(x); }
 
 // Register-array access with a runtime index, lowered to a select chain so the
 // array itself stays in VGPRs (a dynamic subscript would demote it to scratch).
+// The empty asm pins each element as a register value: without it InstCombine
+// folds the select chain back into one dynamically indexed load (a[i]), which
+// forces the whole enclosing aggregate (the column struct) into scratch.
+template <class T>
+__device__ __forceinline__ T pin(T v) {
+  __asm__ volatile("" : "+v"(v));
+  return v;
+}
 template <class T, int N>
 __device__ __forceinline__ T dget(const T (&a)[N], int i) {
-  T r = a[0];
+  T r = pin(a[0]);
 #pragma unroll
-  for (int k = 1; k < N; ++k) r = (i == k) ? a[k] : r;
+  for (int k = 1; k < N; ++k) r = (i == k) ? pin(a[k]) : r;
   return r;
 }
 template <class T, int N>

@@ -167,3 +167,15 @@ def test_case_generator_consistency(ref_params, kind):
     assert (sh2o <= smc + 1e-7).all()
     f = cases.forcing_step(cols, 180.0, 366, 0, seed=1)
     assert f.shape == (L.NFORCING, cols.n) and np.isfinite(f).all()
+
+
+def test_kernel_emits_every_output_once():
+    """Static check of csrc/sflx_kernel.hip: every NMP_D_* diagnostic is emitted
+    exactly once through the output sink and every state field is stored."""
+    from collections import Counter
+    src = open(os.path.join(ROOT, "noahmp-1_amd", "csrc", "sflx_kernel.hip")).read()
+    c = Counter(re.findall(r"d<NMP_D_(\w+)>", src))
+    assert {d for d in L.DIAG_FULL if c[d] != 1} == set(), c
+    stored = set(re.findall(r"out\.s\(NMP_S_(\w+)", src)) | set(
+        re.findall(r"so\[\(?NMP_S_(\w+)", src))
+    assert {n for n, _ in L.STATE_FIELDS} <= stored

@@ -1,0 +1,25 @@
+"""Build tuning variants of the engine library into noahmp-1_amd/lib/variants/."""
+import os
+import sys
+from concurrent.futures import ThreadPoolExecutor
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import noahmp_pkg  # noqa: E402,F401
+from noahmp_amd import build  # noqa: E402
+
+VARIANTS = {
+    "base": (),
+    "w2": ("-DNMP_WAVES_PER_EU=2",),
+    "outline": ("-DNMP_MATH_OUTLINE",),
+    "outline_w2": ("-DNMP_MATH_OUTLINE", "-DNMP_WAVES_PER_EU=2"),
+    "w4": ("-DNMP_WAVES_PER_EU=4",),
+}
+if __name__ == "__main__":
+    names = sys.argv[1:] or list(VARIANTS)
+    vdir = os.path.join(build.LIB_DIR, "variants")
+    with ThreadPoolExecutor(4) as ex:
+        list(ex.map(lambda n: build.build(force=True, verbose=False,
+                                          out=os.path.join(vdir, f"lib_{n}.so"),
+                                          extra=VARIANTS[n]), names))
+    print("built", names)

@@ -59,7 +59,10 @@ def main():
     bw, _ = mean_for(os.path.join(base, "bench_WRITE_SIZE"), "WRITE_SIZE", KERNEL)
     rd = bf * 1024.0 * rf
     wr = bw * 1024.0 * rw
-    res = {"ncol": ncol, "precision": 4, "math": "ref", "kernel": KERNEL, "dispatches": nb,
+    sys.path.insert(0, ROOT)
+    import noahmp_pkg  # noqa: F401
+    from noahmp_amd import build
+    res = {"source_hash": build.source_hash(), "ncol": ncol, "precision": 4, "math": "ref", "kernel": KERNEL, "dispatches": nb,
            "fetch_size_kb": bf, "write_size_kb": bw, "read_correction": rf,
            "write_correction": rw, "read_bytes": rd, "write_bytes": wr,
            "bytes_per_launch": rd + wr, "bytes_per_colstep": (rd + wr) / ncol,
