@@ -30,7 +30,7 @@ sys.path.insert(0, ROOT)
 import numpy as np  # noqa: E402
 
 import noahmp_pkg  # noqa: E402,F401
-from noahmp_amd import cases, layout as L  # noqa: E402
+from noahmp_amd import cases, layout as L, shard  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E, /opt/skills/guides/MI355X_MICROARCH.md
 METRIC = BASELINE_METRIC = "land-columns·timesteps/sec at 4 soil + 3 snow layers, 1/2/4/8 MI355X"
@@ -130,7 +130,7 @@ def main():
         if out and world > 1:
             comm.wait_stream(compute)
             with torch.cuda.stream(comm):
-                pending[b] = dist.all_gather_into_tensor(gathered[b], diag[b], async_op=True)
+                _, pending[b] = shard.gather_diag(diag[b], gathered[b], async_op=True)
         return out
 
     for k in range(a.warmup):

@@ -1,0 +1,80 @@
+"""Multi-rank path on CPU (gloo, world_size 2): column sharding + the
+output-step diagnostics all-gather reproduce the single-rank result bit for
+bit (SURVEY.md 8e correctness test).  Per-shard physics is computed by the
+oracle restatement (this is a test of the sharding plumbing)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+import noahmp_pkg  # noqa: F401,E402  (spawned ranks re-import this module)
+from noahmp_amd import layout as L, shard  # noqa: E402
+
+
+def test_shard_range_partitions():
+    for n in (0, 1, 7, 1024, 1000003):
+        for w in (1, 2, 3, 8):
+            got = [shard.shard_range(n, r, w) for r in range(w)]
+            assert sum(c for _, c in got) == n
+            assert all(got[r][0] + got[r][1] == got[r + 1][0] for r in range(w - 1))
+            assert max(c for _, c in got) - min(c for _, c in got) <= 1
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, out_path):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root, os.path.join(root, "oracle"), os.path.join(root, "tests")]
+    import noahmp_pkg  # noqa: F401
+    import port as oracle
+    from golden_io import load, load_params
+    from noahmp_amd import shard as sh
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    g = load("single_casenml_mixed.npz")
+    n = g["isnow0"].shape[0]
+    s0, cnt = sh.shard_range(n, rank, world)
+    sl = slice(s0, s0 + cnt)
+    _, _, dg, _ = oracle.step(load_params(), tuple(g["options"]), g["zsoil"], float(g["dt"]),
+                              int(g["yearlen"]), float(g["julian"]), g["state0"][:, sl],
+                              g["isnow0"][sl], g["static_f"][:, sl], g["static_i"][:, sl],
+                              g["forcing"][:, sl])
+    idx = [L.DIAG_FULL.index(d) if d != "T2M" else L.DIAG_FULL.index("T2MV") for d in L.DIAG_OUT]
+    local = torch.from_numpy(np.ascontiguousarray(dg[idx]))
+    out, work = sh.gather_diag(local, async_op=True)
+    work.wait()
+    if rank == 0:
+        np.save(out_path, out.numpy())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_gloo_two_rank_gather_equals_single_rank(oracle_port, tmp_path):
+    from golden_io import load, load_params
+    world, port = 2, _free_port()
+    out_path = str(tmp_path / "gathered.npy")
+    mp.start_processes(_worker, args=(world, port, out_path), nprocs=world, start_method="spawn")
+    got = np.load(out_path)
+    g = load("single_casenml_mixed.npz")
+    _, _, dg, _ = oracle_port.step(load_params(), tuple(g["options"]), g["zsoil"],
+                                   float(g["dt"]), int(g["yearlen"]), float(g["julian"]),
+                                   g["state0"], g["isnow0"], g["static_f"], g["static_i"],
+                                   g["forcing"])
+    idx = [L.DIAG_FULL.index(d) if d != "T2M" else L.DIAG_FULL.index("T2MV") for d in L.DIAG_OUT]
+    full = dg[idx]
+    n = full.shape[1]
+    per = n // world
+    rebuilt = np.concatenate([got[r * L.NDIAG_OUT:(r + 1) * L.NDIAG_OUT] for r in range(world)],
+                             axis=1)
+    assert rebuilt.shape == full.shape and per * world == n
+    assert np.array_equal(rebuilt, full) or np.array_equal(
+        np.nan_to_num(rebuilt, nan=1e30), np.nan_to_num(full, nan=1e30))
