@@ -16,7 +16,7 @@ CSRC = os.path.join(PKG, "csrc")
 LIB_DIR = os.path.join(PKG, "lib")
 LIB_PATH = os.environ.get("NOAHMP_ENGINE_LIB") or os.path.join(LIB_DIR, "libnoahmp_engine.so")
 SOURCES = ["engine.hip", "sflx_kernel.hip", "tables.cpp"]
-HEADERS = ["dev_params.h", "sflx_kargs.h", "sflx_math.h"]
+HEADERS = ["dev_params.h", "sflx_kargs.h", "sflx_math.h", "glibc_math.h"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")
 FLAGS = ["-O3", f"--offload-arch={ARCH}", "-fPIC", "-shared", "-std=c++17",

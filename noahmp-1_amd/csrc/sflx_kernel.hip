@@ -760,6 +760,15 @@ struct Sink {
   T* st;        // state + column
   int64_t ld;
   int level;
+  const T* sf;        // static_f + column
+  const int32_t* si;  // static_i + column
+  const T* fc;        // forcing + column
+  // late loads: fields first needed deep in the step are read there, not at
+  // kernel entry, so they do not hold registers through the energy phase
+  DEV T ls(int f) const { return st[f * ld]; }
+  DEV T lf(int f) const { return sf[f * ld]; }
+  DEV int li(int f) const { return si[f * ld]; }
+  DEV T la(int f) const { return fc[f * ld]; }
   template <int D>
   DEV void d(T v) const {
     if (level == NMP_DIAG_FULL) {
@@ -775,9 +784,32 @@ struct Sink {
   DEV void s(int f, T v) const { st[f * ld] = v; }
 };
 
+// Optional per-phase timing (build with -DNMP_PHASE_TIMING; tools only):
+// each wave stamps s_memtime at phase boundaries and lane 0 accumulates the
+// deltas into nmp_phase_cycles[phase].  Compiled out otherwise.
+#ifdef NMP_PHASE_TIMING
+__device__ unsigned long long nmp_phase_cycles[16];
+struct PhaseClock {
+  unsigned long long t;
+  int ph;
+  DEV void mark(int next) {
+    const unsigned long long now = __builtin_amdgcn_s_memtime();
+    if ((threadIdx.x & 63) == 0) atomicAdd(&nmp_phase_cycles[ph], now - t);
+    t = now;
+    ph = next;
+  }
+};
+#define NMP_PHASE(i) pclk.mark(i)
+#else
+#define NMP_PHASE(i) ((void)0)
+#endif
+
 template <class T, bool R>
 DEV void sflx_column(const DevParams& P, const KArgs<T>& A, Col<T>& c, const Sink<T>& out) {
   typedef Mth<T, R> M;
+#ifdef NMP_PHASE_TIMING
+  PhaseClock pclk{__builtin_amdgcn_s_memtime(), 0};
+#endif
   const Opt& o = A.o;
   const VegRec& V = P.veg[c.lutyp - 1];
   const SoilRec& S = P.soil[c.sltyp - 1];
@@ -912,6 +944,7 @@ DEV void sflx_column(const DevParams& P, const KArgs<T>& A, Col<T>& c, const Sin
   if (zpdg >= zlvl) zlvl = zpdg + c.zref;
   const T cwp = (T)V.cwpvt;
 
+  NMP_PHASE(1);
   // thermoprop + csnow + tdfcnd: func.f90:1341-1595
 #pragma unroll
   for (int j = 0; j < 3; ++j) {
@@ -953,6 +986,7 @@ DEV void sflx_column(const DevParams& P, const KArgs<T>& A, Col<T>& c, const Sin
   else
     c.df[3] = (c.df[3] * c.dz[3] + c.df[2] * c.dz[2]) / (c.dz[2] + c.dz[3]);
 
+  NMP_PHASE(2);
   // radiation: albedo + twostream + surrad (func.f90:1598-2005)
   T albgrd[2] = {L(0.), L(0.)}, albgri[2] = {L(0.), L(0.)}, albd[2] = {L(0.), L(0.)};
   T albi[2] = {L(0.), L(0.)}, fabd[2] = {L(0.), L(0.)}, fabi[2] = {L(0.), L(0.)};
@@ -1092,6 +1126,7 @@ DEV void sflx_column(const DevParams& P, const KArgs<T>& A, Col<T>& c, const Sin
     emg = (T)P.g.emssoil * (L(1.0) - fsno) + L(1.0) * fsno;
   else
     emg = (T)P.g.emslake * (L(1.0) - fsno) + L(1.0) * fsno;
+  NMP_PHASE(3);
   // soil moisture stress (:1117-1140)
   T btran = L(0.0);
 #pragma unroll
@@ -1145,6 +1180,12 @@ DEV void sflx_column(const DevParams& P, const KArgs<T>& A, Col<T>& c, const Sin
   const T gammag = CPAIR * c.sfcprs / (L(0.622) * latheag);
   const T stc_top = dget(c.stc, kt), df_top = dget(c.df, kt), dz_top = dget(c.dz, kt);
 
+  // fields first used by the flux phase
+  c.tah = out.ls(NMP_S_TAH); c.eah = out.ls(NMP_S_EAH); c.canliq = out.ls(NMP_S_CANLIQ);
+  c.canice = out.ls(NMP_S_CANICE); c.qsfc = out.ls(NMP_S_QSFC); c.cm = out.ls(NMP_S_CM);
+  c.ch = out.ls(NMP_S_CH); c.tbot = out.lf(NMP_F_TBOT); c.foln = out.lf(NMP_F_FOLN);
+  c.co2air = out.la(NMP_A_CO2AIR); c.o2air = out.la(NMP_A_O2AIR);
+  NMP_PHASE(4);
   // ---- vege_flux: func.f90:2465-2964 ----
   T tgv = L(0.0), cmv = L(0.0);
   if (veg && fveg > L(0.0)) {
@@ -1291,6 +1332,7 @@ DEV void sflx_column(const DevParams& P, const KArgs<T>& A, Col<T>& c, const Sin
     chuc = L(1.0) / rahg;
   }
 
+  NMP_PHASE(5);
   // ---- bare_flux: func.f90:2967-3257 ----
   T tgb = c.tg, cmb = c.cm, chb = c.ch;
   T irb, shb, evb, ghb, t2mb = L(0.0), q2b = L(0.0), chb2 = L(0.0);
@@ -1366,6 +1408,7 @@ DEV void sflx_column(const DevParams& P, const KArgs<T>& A, Col<T>& c, const Sin
     chb = ehb;
   }
 
+  NMP_PHASE(6);
   // tile aggregation (:1246-1282)
   T fira, fsh, fgev, ssoil, fcev, fctr, t2m;
   if (veg && fveg > L(0.0)) {
@@ -1446,6 +1489,7 @@ DEV void sflx_column(const DevParams& P, const KArgs<T>& A, Col<T>& c, const Sin
   out.s(NMP_S_CM, c.cm);
   out.s(NMP_S_CH, c.ch);
 
+  NMP_PHASE(7);
   // tsnosoi + hrt + hstep (func.f90:3987-4237), layers kt..6 in VGPRs
   {
     T ai[7], bi[7], ci[7], rhs[7], ddz[7], denom[7], dtsdz[7];
@@ -1527,6 +1571,7 @@ DEV void sflx_column(const DevParams& P, const KArgs<T>& A, Col<T>& c, const Sin
   out.template d<NMP_D_TGV>(tgv);
   out.s(NMP_S_TG, c.tg);
 
+  NMP_PHASE(8);
   // phasechange: func.f90:4291-4491
   T qmelt = L(0.0), ponding = L(0.0);
   {
@@ -1694,7 +1739,14 @@ DEV void sflx_column(const DevParams& P, const KArgs<T>& A, Col<T>& c, const Sin
   out.template d<NMP_D_EDIR>(edir);
   out.s(NMP_S_SNEQVO, c.sneqvo);
 
+  NMP_PHASE(9);
   // ===================== water: func.f90:4601-4804 =====================
+  // fields first used by the water / carbon phase
+  c.zwt = out.ls(NMP_S_ZWT); c.wa = out.ls(NMP_S_WA); c.wt = out.ls(NMP_S_WT);
+  c.wslake = out.ls(NMP_S_WSLAKE); c.lfmass = out.ls(NMP_S_LFMASS);
+  c.rtmass = out.ls(NMP_S_RTMASS); c.stmass = out.ls(NMP_S_STMASS); c.wood = out.ls(NMP_S_WOOD);
+  c.stblcp = out.ls(NMP_S_STBLCP); c.fastcp = out.ls(NMP_S_FASTCP);
+  c.slptyp = out.li(NMP_I_SLOPETYP);
   T ecan, etran, runsrf = L(0.0), runsub = L(0.0), qsnbot = L(0.0), ponding1 = L(0.0);
   T ponding2 = L(0.0), fpice = L(0.0), snoflow = L(0.0);
   T qrain, snowhin;
@@ -1796,6 +1848,7 @@ DEV void sflx_column(const DevParams& P, const KArgs<T>& A, Col<T>& c, const Sin
   T qsnfro = (c.sneqv > L(0.0)) ? qdew : L(0.0);
   T qsdew = qdew - qsnfro;
 
+  NMP_PHASE(10);
   // snowwater: func.f90:5049-5174.  Two passes share one copy of `combine`:
   // pass 0 = snowfall + compact + combine, pass 1 = divide + snowh2o head +
   // its conditional combine.
@@ -1995,6 +2048,7 @@ DEV void sflx_column(const DevParams& P, const KArgs<T>& A, Col<T>& c, const Sin
     for (int k = 0; k < 7; ++k)
       if (k >= kt2) c.dz[k] = -c.dz[k];
   }
+  NMP_PHASE(11);
   // frozen ground (:4744-4752)
   if (frozen_ground) {
     c.sice[0] = c.sice[0] + (qsdew - qseva) * DT / (c.dz[3] * L(1000.0));
@@ -2020,6 +2074,7 @@ DEV void sflx_column(const DevParams& P, const KArgs<T>& A, Col<T>& c, const Sin
     if (c.wslake >= L(5000.)) runsrf = qinsrf * L(1000.0);
     c.wslake = c.wslake + (qinsrf - qseva) * L(1000.0) * DT - runsrf * DT;
   } else {
+    NMP_PHASE(12);
     // soilh2o: func.f90:5822-6048
     T wcnd[4], fcr[4];
     T qdrain = L(0.0), fcrmax = L(0.0);
@@ -2357,6 +2412,7 @@ DEV void sflx_column(const DevParams& P, const KArgs<T>& A, Col<T>& c, const Sin
   out.template d<NMP_D_PONDING1>(ponding1);
   out.template d<NMP_D_PONDING2>(ponding2);
 
+  NMP_PHASE(13);
   // carbon + co2flux (opt_veg 2|5): func.f90:6642-7025
   T gpp = L(0.0), npp = L(0.0), nee = L(0.0);
   if (o.veg == 2 || o.veg == 5) {
@@ -2460,6 +2516,7 @@ DEV void sflx_column(const DevParams& P, const KArgs<T>& A, Col<T>& c, const Sin
     c.sneqv = L(0.0);
   }
   out.template d<NMP_D_Q2B>(q2b);
+  NMP_PHASE(15);
 }
 
 // ---------------------------------------------------------------------------
@@ -2480,6 +2537,7 @@ void sflx_step_kernel(const DevParams* __restrict__ gparams,
     constexpr int NW = sizeof(DevParams) / sizeof(int4);
     for (int i = threadIdx.x; i < NW; i += blockDim.x) dst[i] = src[i];
   }
+  if constexpr (sizeof(T) == 4 && R) stage_math_tables();
   __syncthreads();
   const int64_t c0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (c0 >= a.ncol) return;
@@ -2501,32 +2559,27 @@ void sflx_step_kernel(const DevParams* __restrict__ gparams,
     c.sh2o[k] = st[(NMP_S_SH2O + k) * ld];
     c.smc[k] = st[(NMP_S_SMC + k) * ld];
   }
-  c.tv = st[NMP_S_TV * ld]; c.tg = st[NMP_S_TG * ld]; c.tah = st[NMP_S_TAH * ld];
-  c.eah = st[NMP_S_EAH * ld]; c.fwet = st[NMP_S_FWET * ld]; c.canliq = st[NMP_S_CANLIQ * ld];
-  c.canice = st[NMP_S_CANICE * ld]; c.qsfc = st[NMP_S_QSFC * ld]; c.snowh = st[NMP_S_SNOWH * ld];
+  c.tv = st[NMP_S_TV * ld]; c.tg = st[NMP_S_TG * ld];
+  c.fwet = st[NMP_S_FWET * ld]; c.snowh = st[NMP_S_SNOWH * ld];
   c.sneqv = st[NMP_S_SNEQV * ld]; c.sneqvo = st[NMP_S_SNEQVO * ld];
   c.albold = st[NMP_S_ALBOLD * ld]; c.tauss = st[NMP_S_TAUSS * ld];
-  c.qsnow = st[NMP_S_QSNOW * ld]; c.zwt = st[NMP_S_ZWT * ld]; c.wa = st[NMP_S_WA * ld];
-  c.wt = st[NMP_S_WT * ld]; c.wslake = st[NMP_S_WSLAKE * ld]; c.lai = st[NMP_S_LAI * ld];
-  c.sai = st[NMP_S_SAI * ld]; c.lfmass = st[NMP_S_LFMASS * ld]; c.rtmass = st[NMP_S_RTMASS * ld];
-  c.stmass = st[NMP_S_STMASS * ld]; c.wood = st[NMP_S_WOOD * ld]; c.stblcp = st[NMP_S_STBLCP * ld];
-  c.fastcp = st[NMP_S_FASTCP * ld]; c.cm = st[NMP_S_CM * ld]; c.ch = st[NMP_S_CH * ld];
+  c.qsnow = st[NMP_S_QSNOW * ld]; c.lai = st[NMP_S_LAI * ld]; c.sai = st[NMP_S_SAI * ld];
   c.isnow = a.isnow[c0];
   const T* sf = a.static_f + c0;
   c.lat = sf[NMP_F_LAT * ld]; c.zref = sf[NMP_F_ZLVL * ld]; c.shdfac = sf[NMP_F_SHDFAC * ld];
-  c.shdmax = sf[NMP_F_SHDMAX * ld]; c.tbot = sf[NMP_F_TBOT * ld]; c.foln = sf[NMP_F_FOLN * ld];
+  c.shdmax = sf[NMP_F_SHDMAX * ld];
   const int32_t* si = a.static_i + c0;
   c.lutyp = si[NMP_I_VEGTYP * ld]; c.sltyp = si[NMP_I_SOILTYP * ld];
-  c.slptyp = si[NMP_I_SLOPETYP * ld]; c.isc = si[NMP_I_SOILCOLOR * ld];
+  c.isc = si[NMP_I_SOILCOLOR * ld];
   c.ist = si[NMP_I_IST * ld]; c.ice = si[NMP_I_ICE * ld];
   const T* fc = a.forcing + c0;
   c.sfctmp = fc[NMP_A_SFCTMP * ld]; c.sfcprs = fc[NMP_A_SFCPRS * ld]; c.psfc = fc[NMP_A_PSFC * ld];
   c.uu = fc[NMP_A_UU * ld]; c.vv = fc[NMP_A_VV * ld]; c.q2 = fc[NMP_A_Q2 * ld];
   c.soldn = fc[NMP_A_SOLDN * ld]; c.lwdn = fc[NMP_A_LWDN * ld]; c.prcp = fc[NMP_A_PRCP * ld];
-  c.cosz = fc[NMP_A_COSZ * ld]; c.co2air = fc[NMP_A_CO2AIR * ld]; c.o2air = fc[NMP_A_O2AIR * ld];
+  c.cosz = fc[NMP_A_COSZ * ld];
   c.status = 0;
 
-  const Sink<T> out{a.diag ? a.diag + c0 : nullptr, a.state + c0, ld, a.diag_level};
+  const Sink<T> out{a.diag ? a.diag + c0 : nullptr, a.state + c0, ld, a.diag_level, sf, si, fc};
   sflx_column<T, R>(sp, a, c, out);
 
   T* so = a.state + c0;
@@ -2569,6 +2622,18 @@ hipError_t launch_sflx(const DevParams* dparams, const KArgs<T>& a, hipStream_t 
   return hipGetLastError();
 }
 
+#ifdef NMP_PHASE_TIMING
+extern "C" int nmp_debug_phase_cycles(unsigned long long* out16, int reset) {
+  if (hipMemcpyFromSymbol(out16, HIP_SYMBOL(nmp_phase_cycles), sizeof(unsigned long long) * 16) !=
+      hipSuccess)
+    return -4;
+  if (reset) {
+    unsigned long long z[16] = {0};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(nmp_phase_cycles), z, sizeof(z)) != hipSuccess) return -4;
+  }
+  return 0;
+}
+#endif
 template hipError_t launch_sflx<float, true>(const DevParams*, const KArgs<float>&, hipStream_t);
 template hipError_t launch_sflx<float, false>(const DevParams*, const KArgs<float>&, hipStream_t);
 template hipError_t launch_sflx<double, false>(const DevParams*, const KArgs<double>&, hipStream_t);

@@ -1,11 +1,12 @@
 // Arithmetic helpers for the sflx kernel (device side).
 //
 // Transcendental policy:
-//  - Mth<float, true>  "ref":  float functions evaluated in double and rounded once to
-//    float.  glibc's float functions used by the reference (compiled by
-//    amdflang, core/module_noahmp_func.f90) are correctly rounded or within
-//    ~0.5-0.8 ulp, so this policy reproduces their results in all but rare
-//    near-midpoint cases.  Parity mode.
+//  - Mth<float, true>  "ref":  bit-exact restatements of the glibc 2.35 float
+//    libm the reference's compiled physics calls (glibc_math.h: expf, exp2f,
+//    logf, powf, tanhf, atanf, log10f, acosf, cosf, tanf).  Each is checked
+//    against the host libm over all 2^32 inputs (powf: 26e9 samples), so the
+//    kernel's elementary functions return exactly what the reference's do.
+//    Their small tables (768 B) are staged per workgroup in LDS.  Default.
 //  - Mth<float, false> "fast": ocml single-precision functions (<= ~1-2 ulp).
 //  - Mth<double, *>:          ocml double functions (fp64 engine).
 // Division and sqrt are IEEE correctly rounded in every policy (hipcc default
@@ -14,6 +15,8 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <math.h>
+
+#include "glibc_math.h"
 
 // Math wrappers are inlined by default; -DNMP_MATH_OUTLINE keeps one copy of
 // each (smaller code, fewer instruction-cache misses, call overhead instead).
@@ -58,20 +61,31 @@ struct Mth<float, false> {
   static __device__ __forceinline__ float sqrt(float x) { return ::sqrtf(x); }
 };
 
+// glibc libm tables: one __constant__ master copy, staged into LDS by every
+// workgroup's prologue (stage_math_tables) before first use.
+__shared__ gm::GmTables gm_lds;
+__constant__ gm::GmTables gm_const = {GM_EXP2F_TAB, GM_LOGF_TAB, GM_POWF_TAB};
+
+__device__ __forceinline__ void stage_math_tables() {
+  constexpr int NW = sizeof(gm::GmTables) / sizeof(int4);
+  static_assert(sizeof(gm::GmTables) % sizeof(int4) == 0, "table size");
+  const int4* src = reinterpret_cast<const int4*>(&gm_const);
+  int4* dst = reinterpret_cast<int4*>(&gm_lds);
+  for (int i = threadIdx.x; i < NW; i += blockDim.x) dst[i] = src[i];
+}
+
 template <>
 struct Mth<float, true> {
-  NMP_MATH_FN float exp(float x) { return (float)::exp((double)x); }
-  NMP_MATH_FN float exp2(float x) { return (float)::exp2((double)x); }
-  NMP_MATH_FN float log(float x) { return (float)::log((double)x); }
-  NMP_MATH_FN float log10(float x) { return (float)::log10((double)x); }
-  NMP_MATH_FN float pow(float x, float y) {
-    return (float)::pow((double)x, (double)y);
-  }
-  NMP_MATH_FN float tanh(float x) { return (float)::tanh((double)x); }
-  NMP_MATH_FN float atan(float x) { return (float)::atan((double)x); }
-  NMP_MATH_FN float tan(float x) { return (float)::tan((double)x); }
-  NMP_MATH_FN float acos(float x) { return (float)::acos((double)x); }
-  NMP_MATH_FN float cos(float x) { return (float)::cos((double)x); }
+  NMP_MATH_FN float exp(float x) { return gm::expf(x, gm_lds); }
+  NMP_MATH_FN float exp2(float x) { return gm::exp2f(x, gm_lds); }
+  NMP_MATH_FN float log(float x) { return gm::logf(x, gm_lds); }
+  NMP_MATH_FN float log10(float x) { return gm::log10f(x, gm_lds); }
+  NMP_MATH_FN float pow(float x, float y) { return gm::powf(x, y, gm_lds); }
+  NMP_MATH_FN float tanh(float x) { return gm::tanhf(x); }
+  NMP_MATH_FN float atan(float x) { return gm::atanf(x); }
+  NMP_MATH_FN float tan(float x) { return gm::tanf(x); }
+  NMP_MATH_FN float acos(float x) { return gm::acosf(x); }
+  NMP_MATH_FN float cos(float x) { return gm::cosf(x); }
   static __device__ __forceinline__ float sqrt(float x) { return ::sqrtf(x); }
 };
 

@@ -14,6 +14,8 @@ VARIANTS = {
     "outline": ("-DNMP_MATH_OUTLINE",),
     "outline_w2": ("-DNMP_MATH_OUTLINE", "-DNMP_WAVES_PER_EU=2"),
     "w4": ("-DNMP_WAVES_PER_EU=4",),
+    "w1": ("-DNMP_WAVES_PER_EU=1",),
+    "phase": ("-DNMP_PHASE_TIMING",),
 }
 if __name__ == "__main__":
     names = sys.argv[1:] or list(VARIANTS)
