@@ -51,6 +51,9 @@ def parse():
     ap.add_argument("--steps", type=int, default=48)
     ap.add_argument("--warmup", type=int, default=4)
     ap.add_argument("--ncol", type=int, default=1 << 20, help="columns per GPU")
+    ap.add_argument("--kind", default="mixed", choices=("mixed", "conus", "casenml"),
+                    help="column set: mixed (config #3), conus (config #4 types), casenml "
+                         "(replicated run/case.nml column, config #2)")
     ap.add_argument("--precision", type=int, default=4, choices=(4, 8))
     ap.add_argument("--math", default="ref", choices=("ref", "fast"))
     ap.add_argument("--dt", type=float, default=1800.0)
@@ -75,7 +78,7 @@ def main():
     pdict = P.as_dict()
     options = L.options_tuple(L.CASE_NML_OPTIONS)
     julian0, yearlen, seed = 180.0, 366, 1000 + rank
-    cols = cases.make_columns(a.ncol, "mixed", pdict, seed=seed, julian=julian0)
+    cols = cases.make_columns(a.ncol, a.kind, pdict, seed=seed, julian=julian0)
 
     # ---- CPU baseline (rank 0, N=1), BEFORE anything touches the GPU ------
     cpu = None
@@ -184,8 +187,10 @@ def main():
             "dtype": "f32" if a.precision == 4 else "f64",
             "data": "synthetic (seeded mixed USGS/STAS columns, diurnal forcing; no dataset)",
             "config": {"workload": "config #3: 1,048,576 columns/GPU, 4 soil + 3 snow layers, "
-                                   "dynamic_veg off, case.nml options" if n == 1 << 20 else
-                       f"{n} columns/GPU, 4 soil + 3 snow layers", "ncol_per_gpu": n,
+                                   "dynamic_veg off, case.nml options"
+                       if (n == 1 << 20 and a.kind == "mixed") else
+                       f"{n} {a.kind} columns/GPU, 4 soil + 3 snow layers", "kind": a.kind,
+                       "ncol_per_gpu": n,
                        "ncol_total": world * n, "dt_s": a.dt, "out_every": a.out_every,
                        "math": a.math, "parallelism": f"column-shard x{world}"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",

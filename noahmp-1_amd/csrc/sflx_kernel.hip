@@ -223,17 +223,30 @@ DEV void twostream(const DevParams& P, const VegRec& V, const Opt& o, int ib, in
 }
 
 // sfcdif1: func.f90:3353-3508
+// The four log terms of sfcdif1 (:3417-3420) depend only on heights fixed for
+// the whole Newton loop; callers evaluate them once (same values, bit for bit)
+// instead of once per iteration as the reference does.
 template <class T, bool R>
-DEV void sfcdif1(int iter, T sfctmp, T rhoair, T h, T qair, T zlvl, T zpd, T z0m, T z0h, T ur,
-                 T mpe, T& moz, int& mozsgn, T& fm, T& fh, T& fm2, T& fh2, T& cm, T& ch, T& fv,
-                 int& status) {
+struct Sfc1Logs {
+  T tmpcm, tmpch, tmpcm2, tmpch2;
+  DEV Sfc1Logs() : tmpcm(0), tmpch(0), tmpcm2(0), tmpch2(0) {}
+  DEV Sfc1Logs(T zlvl, T zpd, T z0m, T z0h, int& status) {
+    typedef Mth<T, R> M;
+    if (zlvl <= zpd) status |= NMP_ST_ZLVL;  // :3412-3415
+    tmpcm = M::log((zlvl - zpd) / z0m);
+    tmpch = (z0h == z0m) ? tmpcm : M::log((zlvl - zpd) / z0h);
+    tmpcm2 = M::log((L(2.0) + z0m) / z0m);
+    tmpch2 = (z0h == z0m) ? tmpcm2 : M::log((L(2.0) + z0h) / z0h);
+  }
+};
+
+template <class T, bool R>
+DEV void sfcdif1(int iter, T sfctmp, T rhoair, T h, T qair, T zlvl, T zpd, const Sfc1Logs<T, R>& lg,
+                 T z0h, T ur, T mpe, T& moz, int& mozsgn, T& fm, T& fh, T& fm2, T& fh2, T& cm,
+                 T& ch, T& fv) {
   typedef Mth<T, R> M;
   T mozold = moz;
-  if (zlvl <= zpd) status |= NMP_ST_ZLVL;
-  T tmpcm = M::log((zlvl - zpd) / z0m);
-  T tmpch = M::log((zlvl - zpd) / z0h);
-  T tmpcm2 = M::log((L(2.0) + z0m) / z0m);
-  T tmpch2 = M::log((L(2.0) + z0h) / z0h);
+  const T tmpcm = lg.tmpcm, tmpch = lg.tmpch, tmpcm2 = lg.tmpcm2, tmpch2 = lg.tmpch2;
   T moz2;
   if (iter == 1) {
     fv = L(0.0);
@@ -381,8 +394,8 @@ DEV void sfcdif2(int iter, T z0, T thz0, T thlm, T sfcspd, T czil, T zlm, T& akm
 
 // ragrb: func.f90:3260-3350
 template <class T, bool R>
-DEV void ragrb(const VegRec& V, int iter, T vai, T rhoair, T hg, T tah, T zpd, T z0mg, T z0hg,
-               T hcan, T uc, T z0h, T fv, T cwp, T mpe, T& fhg, T& rahg, T& rb) {
+DEV void ragrb(T sqrt_dleaf_uc, int iter, T vai, T rhoair, T hg, T tah, T zpd, T z0mg, T z0hg,
+               T hcan, T z0h, T fv, T cwp, T mpe, T& fhg, T& rahg, T& rb) {
   typedef Mth<T, R> M;
   T mozg = L(0.0);
   if (iter > 1) {
@@ -400,7 +413,7 @@ DEV void ragrb(const VegRec& V, int iter, T vai, T rhoair, T hg, T tah, T zpd, T
   T kh = rmax(KARMAN * fv * (hcan - zpd), mpe);
   rahg = tmprah2 / kh;
   T tmprb = cwpc * L(50.0) / (L(1.0) - M::exp(-cwpc / L(2.0)));
-  rb = tmprb * M::sqrt((T)V.dleaf / uc);
+  rb = tmprb * sqrt_dleaf_uc;
 }
 
 // stomata (Ball-Berry bisection): func.f90:3739-3887
@@ -743,6 +756,21 @@ DEV void divide(Col<T>& c) {
 
 // ---------------------------------------------------------------------------
 // noahmp_sflx for one column: func.f90:66-476
+// layer thickness DZSNSO from the layer-bottom depths (func.f90:322-328)
+template <class T>
+DEV void layer_dz(Col<T>& c) {
+#pragma unroll
+  for (int k = 0; k < 7; ++k) {
+    const int km = k > 0 ? k - 1 : 0;
+    if (k == c.isnow + 3)
+      c.dz[k] = -c.zsnso[k];
+    else if (k > c.isnow + 3)
+      c.dz[k] = c.zsnso[km] - c.zsnso[k];
+    else
+      c.dz[k] = L(0.0);
+  }
+}
+
 // Output sink: diagnostics and final state fields are written to HBM at the
 // point they become final (not held in registers to the end of the step).
 __host__ __device__ constexpr int out_index(int d) {
@@ -766,6 +794,13 @@ struct Sink {
   // late loads: fields first needed deep in the step are read there, not at
   // kernel entry, so they do not hold registers through the energy phase
   DEV T ls(int f) const { return st[f * ld]; }
+  // state pointer laundered through an empty asm: loads through it are real
+  // re-reads, never forwarded from values loaded earlier in the step
+  DEV const T* fresh_state() const {
+    const T* p = st;
+    __asm__ volatile("" : "+v"(p));
+    return p;
+  }
   DEV T lf(int f) const { return sf[f * ld]; }
   DEV int li(int f) const { return si[f * ld]; }
   DEV T la(int f) const { return fc[f * ld]; }
@@ -819,34 +854,19 @@ DEV void sflx_column(const DevParams& P, const KArgs<T>& A, Col<T>& c, const Sin
   const T bexp = (T)S.bexp, psisat = (T)S.psisat;
   const int nroot = V.nroot;
 
-  // FICEOLD from the state at step start (offline-driver convention)
-#pragma unroll
-  for (int j = 0; j < 3; ++j)
-    c.ficeold[j] = (j >= c.isnow + 3) ? c.snice[j] / (c.snice[j] + c.snliq[j]) : L(0.0);
-
   // atm: func.f90:479-531
   T pair = c.sfcprs;
   T thair = c.sfctmp * M::pow(c.sfcprs / pair, RAIR / CPAIR);
   T qair = c.q2;
   T eair = qair * c.sfcprs / (L(0.622) + L(0.378) * qair);
   T rhoair = (c.sfcprs - L(0.378) * eair) / (RAIR * c.sfctmp);
-  T qprecc = L(0.10) * c.prcp;
-  T qprecl = L(0.90) * c.prcp;
+  // QPRECC/QPRECL (:517-518) are only used by canwater: formed there from PRCP
   T swdown = (c.cosz <= L(0.0)) ? L(0.0) : c.soldn;
   T solad = swdown * L(0.7) * L(0.5);
   T solai = swdown * L(0.3) * L(0.5);
 
   // layer thickness (:322-328)
-#pragma unroll
-  for (int k = 0; k < 7; ++k) {
-    const int km = k > 0 ? k - 1 : 0;
-    if (k == c.isnow + 3)
-      c.dz[k] = -c.zsnso[k];
-    else if (k > c.isnow + 3)
-      c.dz[k] = c.zsnso[km] - c.zsnso[k];
-    else
-      c.dz[k] = L(0.0);
-  }
+  layer_dz(c);
   // root-zone temperature (:332-335)
   T troot = L(0.0);
   {
@@ -945,46 +965,20 @@ DEV void sflx_column(const DevParams& P, const KArgs<T>& A, Col<T>& c, const Sin
   const T cwp = (T)V.cwpvt;
 
   NMP_PHASE(1);
-  // thermoprop + csnow + tdfcnd: func.f90:1341-1595
-#pragma unroll
-  for (int j = 0; j < 3; ++j) {
-    if (j >= kt) {
-      T snicev = rmin(L(1.0), c.snice[j] / (c.dz[j] * DENICE));
-      T epore = L(1.0) - snicev;
-      T snliqv = rmin(epore, c.snliq[j] / (c.dz[j] * DENWAT));
-      T bdsnoi = (c.snice[j] + c.snliq[j]) / c.dz[j];
-      c.hcpct[j] = CICE * snicev + CWAT * snliqv;
-      c.df[j] = L(3.2217E-6) * p2(bdsnoi);
-    } else {
-      c.hcpct[j] = L(0.0);
-      c.df[j] = L(0.0);
-    }
+  // Top-layer conductivity DF(ISNOW+1) for the flux Newton loops, computed
+  // exactly as thermoprop computes that element (full thermoprop runs after
+  // the fluxes, so its 21 layer values are not held through the iterations).
+  T df_top;
+  if (kt < 3) {  // snow top layer: csnow (:1490)
+    const T sn_ice = dget(c.snice, kt), sn_liq = dget(c.snliq, kt), sn_dz = dget(c.dz, kt);
+    const T bdsnoi = (sn_ice + sn_liq) / sn_dz;
+    df_top = L(3.2217E-6) * p2(bdsnoi);
+  } else {  // soil layer 1 + snow/soil interface (:1400-1444)
+    T df3 = tdfcnd<T, R>(S, c.smc[0], c.sh2o[0]);
+    if (c.lutyp == P.g.isurban) df3 = L(3.24);
+    if (c.ist == 2) df3 = (c.stc[3] > TFRZ) ? TKWAT : TKICE;
+    df_top = (df3 * c.dz[3] + L(0.35) * c.snowh) / (c.snowh + c.dz[3]);
   }
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    T sice = c.smc[k] - c.sh2o[k];
-    c.hcpct[k + 3] = c.sh2o[k] * CWAT + (L(1.0) - smcmax) * (T)P.g.csoil +
-                     (smcmax - c.smc[k]) * CPAIR + sice * CICE;
-    c.df[k + 3] = tdfcnd<T, R>(S, c.smc[k], c.sh2o[k]);
-  }
-  if (c.lutyp == P.g.isurban) {
-#pragma unroll
-    for (int k = 3; k < 7; ++k) c.df[k] = L(3.24);
-  }
-  if (c.ist == 2) {
-#pragma unroll
-    for (int k = 3; k < 7; ++k) {
-      const bool warm = c.stc[k] > TFRZ;
-      c.hcpct[k] = warm ? CWAT : CICE;
-      c.df[k] = warm ? TKWAT : TKICE;
-    }
-  }
-#pragma unroll
-  for (int k = 0; k < 7; ++k) c.fact[k] = (k >= kt) ? DT / (c.hcpct[k] * c.dz[k]) : L(0.0);
-  if (c.isnow == 0)
-    c.df[3] = (c.df[3] * c.dz[3] + L(0.35) * c.snowh) / (c.snowh + c.dz[3]);
-  else
-    c.df[3] = (c.df[3] * c.dz[3] + c.df[2] * c.dz[2]) / (c.dz[2] + c.dz[3]);
 
   NMP_PHASE(2);
   // radiation: albedo + twostream + surrad (func.f90:1598-2005)
@@ -1178,7 +1172,7 @@ DEV void sflx_column(const DevParams& P, const KArgs<T>& A, Col<T>& c, const Sin
   const bool frozen_ground = !(c.tg > TFRZ);
   const T latheag = frozen_ground ? HSUB : HVAP;
   const T gammag = CPAIR * c.sfcprs / (L(0.622) * latheag);
-  const T stc_top = dget(c.stc, kt), df_top = dget(c.df, kt), dz_top = dget(c.dz, kt);
+  const T stc_top = dget(c.stc, kt), dz_top = dget(c.dz, kt);
 
   // fields first used by the flux phase
   c.tah = out.ls(NMP_S_TAH); c.eah = out.ls(NMP_S_EAH); c.canliq = out.ls(NMP_S_CANLIQ);
@@ -1214,11 +1208,14 @@ DEV void sflx_column(const DevParams& P, const KArgs<T>& A, Col<T>& c, const Sin
             emv * emg * SB * p4(tgv);
     T cir = (L(2.0) - emv * (L(1.0) - emg)) * emv * SB;
     T rahc = L(1.0);
+    const T sqrt_dleaf_uc = M::sqrt((T)V.dleaf / uc);  // ragrb :3349, loop-invariant
+    const Sfc1Logs<T, R> lgv = (o.sfc == 1) ? Sfc1Logs<T, R>(zlvl, zpd, z0m, z0h, c.status)
+                                            : Sfc1Logs<T, R>{};
 #pragma unroll 1
     for (int iter = 1; iter <= 20; ++iter) {
       if (o.sfc == 1)
-        sfcdif1<T, R>(iter, c.sfctmp, rhoair, h, qair, zlvl, zpd, z0m, z0h, ur, mpe, moz, mozsgn,
-                      fm, fh, fm2, fh2, cmv, chv, fv, c.status);
+        sfcdif1<T, R>(iter, c.sfctmp, rhoair, h, qair, zlvl, zpd, lgv, z0h, ur, mpe, moz, mozsgn,
+                      fm, fh, fm2, fh2, cmv, chv, fv);
       if (o.sfc == 2) {
         sfcdif2<T, R>(iter, z0m, c.tah, thair, ur, (T)P.g.czil, zlvl, cmv, chv, moz, wstar, fv);
         chv = chv / ur;
@@ -1226,8 +1223,8 @@ DEV void sflx_column(const DevParams& P, const KArgs<T>& A, Col<T>& c, const Sin
       }
       rahc = rmax(L(1.0), L(1.0) / (chv * ur));
       T rawc = rahc;
-      ragrb<T, R>(V, iter, vaie, rhoair, hg, c.tah, zpd, z0mg, z0mg, hcan, uc, z0h, fv, cwp, mpe,
-                  fhg, rahg, rb);
+      ragrb<T, R>(sqrt_dleaf_uc, iter, vaie, rhoair, hg, c.tah, zpd, z0mg, z0mg, hcan, z0h, fv,
+                  cwp, mpe, fhg, rahg, rb);
       T rawg = rahg;
       tt = tdc(c.tv);
       esat(tt, esatw, esati, dsatw, dsati);
@@ -1346,11 +1343,13 @@ DEV void sflx_column(const DevParams& P, const KArgs<T>& A, Col<T>& c, const Sin
     T z0h = z0mg, ehb = L(0.0), csh = L(0.0), cev = L(0.0), estg = L(0.0);
     T esatw, esati, dsatw, dsati;
     irb = shb = evb = ghb = L(0.0);
+    const Sfc1Logs<T, R> lgb = (o.sfc == 1) ? Sfc1Logs<T, R>(zlvl, zpdg, z0mg, z0h, c.status)
+                                            : Sfc1Logs<T, R>{};
 #pragma unroll 1
     for (int iter = 1; iter <= 5; ++iter) {
       if (o.sfc == 1)
-        sfcdif1<T, R>(iter, c.sfctmp, rhoair, h, qair, zlvl, zpdg, z0mg, z0h, ur, mpe, moz,
-                      mozsgn, fm, fh, fm2, fh2, cmb, chb, fv, c.status);
+        sfcdif1<T, R>(iter, c.sfctmp, rhoair, h, qair, zlvl, zpdg, lgb, z0h, ur, mpe, moz,
+                      mozsgn, fm, fh, fm2, fh2, cmb, chb, fv);
       if (o.sfc == 2) {
         sfcdif2<T, R>(iter, z0mg, tgb, thair, ur, (T)P.g.czil, zlvl, cmb, chb, moz, wstar, fv);
         chb = chb / ur;
@@ -1488,6 +1487,73 @@ DEV void sflx_column(const DevParams& P, const KArgs<T>& A, Col<T>& c, const Sin
   out.s(NMP_S_EAH, c.eah);
   out.s(NMP_S_CM, c.cm);
   out.s(NMP_S_CH, c.ch);
+
+  // Re-read the layer state (unchanged in HBM so far) instead of holding it in
+  // registers through the flux iterations; then FICEOLD and thermoprop.
+  {
+    const T* st = out.fresh_state();
+#pragma unroll
+    for (int k = 0; k < 7; ++k) {
+      c.stc[k] = st[(NMP_S_STC + k) * out.ld];
+      c.zsnso[k] = st[(NMP_S_ZSNSO + k) * out.ld];
+    }
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      c.snice[k] = st[(NMP_S_SNICE + k) * out.ld];
+      c.snliq[k] = st[(NMP_S_SNLIQ + k) * out.ld];
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      c.sh2o[k] = st[(NMP_S_SH2O + k) * out.ld];
+      c.smc[k] = st[(NMP_S_SMC + k) * out.ld];
+    }
+    layer_dz(c);
+  }
+  // FICEOLD from the state at step start (offline-driver convention)
+#pragma unroll
+  for (int j = 0; j < 3; ++j)
+    c.ficeold[j] = (j >= c.isnow + 3) ? c.snice[j] / (c.snice[j] + c.snliq[j]) : L(0.0);
+  NMP_PHASE(1);
+  // thermoprop + csnow + tdfcnd: func.f90:1341-1595
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    if (j >= kt) {
+      T snicev = rmin(L(1.0), c.snice[j] / (c.dz[j] * DENICE));
+      T epore = L(1.0) - snicev;
+      T snliqv = rmin(epore, c.snliq[j] / (c.dz[j] * DENWAT));
+      T bdsnoi = (c.snice[j] + c.snliq[j]) / c.dz[j];
+      c.hcpct[j] = CICE * snicev + CWAT * snliqv;
+      c.df[j] = L(3.2217E-6) * p2(bdsnoi);
+    } else {
+      c.hcpct[j] = L(0.0);
+      c.df[j] = L(0.0);
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    T sice = c.smc[k] - c.sh2o[k];
+    c.hcpct[k + 3] = c.sh2o[k] * CWAT + (L(1.0) - smcmax) * (T)P.g.csoil +
+                     (smcmax - c.smc[k]) * CPAIR + sice * CICE;
+    c.df[k + 3] = tdfcnd<T, R>(S, c.smc[k], c.sh2o[k]);
+  }
+  if (c.lutyp == P.g.isurban) {
+#pragma unroll
+    for (int k = 3; k < 7; ++k) c.df[k] = L(3.24);
+  }
+  if (c.ist == 2) {
+#pragma unroll
+    for (int k = 3; k < 7; ++k) {
+      const bool warm = c.stc[k] > TFRZ;
+      c.hcpct[k] = warm ? CWAT : CICE;
+      c.df[k] = warm ? TKWAT : TKICE;
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 7; ++k) c.fact[k] = (k >= kt) ? DT / (c.hcpct[k] * c.dz[k]) : L(0.0);
+  if (c.isnow == 0)
+    c.df[3] = (c.df[3] * c.dz[3] + L(0.35) * c.snowh) / (c.snowh + c.dz[3]);
+  else
+    c.df[3] = (c.df[3] * c.dz[3] + c.df[2] * c.dz[2]) / (c.dz[2] + c.dz[3]);
 
   NMP_PHASE(7);
   // tsnosoi + hrt + hstep (func.f90:3987-4237), layers kt..6 in VGPRs
@@ -1742,6 +1808,9 @@ DEV void sflx_column(const DevParams& P, const KArgs<T>& A, Col<T>& c, const Sin
   NMP_PHASE(9);
   // ===================== water: func.f90:4601-4804 =====================
   // fields first used by the water / carbon phase
+  const T prcp_w = out.la(NMP_A_PRCP), uu_w = out.la(NMP_A_UU), vv_w = out.la(NMP_A_VV);
+  const T qprecc = L(0.10) * prcp_w;  // atm :517-518
+  const T qprecl = L(0.90) * prcp_w;
   c.zwt = out.ls(NMP_S_ZWT); c.wa = out.ls(NMP_S_WA); c.wt = out.ls(NMP_S_WT);
   c.wslake = out.ls(NMP_S_WSLAKE); c.lfmass = out.ls(NMP_S_LFMASS);
   c.rtmass = out.ls(NMP_S_RTMASS); c.stmass = out.ls(NMP_S_STMASS); c.wood = out.ls(NMP_S_WOOD);
@@ -1803,7 +1872,7 @@ DEV void sflx_column(const DevParams& P, const KArgs<T>& A, Col<T>& c, const Sin
       qints = rmin(qints, (maxsno - c.canice) / DT * (L(1.0) - M::exp(-snow * DT / maxsno)));
       qints = rmax(qints, L(0.0));
       T ft = rmax(L(0.0), (c.tv - L(270.15)) / L(1.87E5));
-      T fvw = M::sqrt(c.uu * c.uu + c.vv * c.vv) / L(1.56E5);
+      T fvw = M::sqrt(uu_w * uu_w + vv_w * vv_w) / L(1.56E5);
       qdrips = rmax(L(0.0), c.canice) * (fvw + ft);
       qthros = (L(1.0) - fveg) * snow + (fveg * snow - qints);
     } else {
@@ -2521,10 +2590,10 @@ DEV void sflx_column(const DevParams& P, const KArgs<T>& A, Col<T>& c, const Sin
 
 // ---------------------------------------------------------------------------
 template <class T, bool R>
-// Occupancy target: 2 waves/SIMD for fp32 (256 VGPRs; measured faster than
-// 1 wave with 500 VGPRs and than 3-4 waves with heavy spilling), 1 for fp64.
+// Occupancy target: 3 waves/SIMD for fp32 (168 VGPRs; measured faster than
+// 1-2 waves with fewer spills and than 4 waves; tools/sweep.sh), 1 for fp64.
 #ifndef NMP_WAVES_PER_EU
-#define NMP_WAVES_PER_EU 2
+#define NMP_WAVES_PER_EU 3
 #endif
 __global__ __launch_bounds__(256)
 __attribute__((amdgpu_waves_per_eu(sizeof(T) == 4 ? NMP_WAVES_PER_EU : 1)))
@@ -2575,7 +2644,7 @@ void sflx_step_kernel(const DevParams* __restrict__ gparams,
   const T* fc = a.forcing + c0;
   c.sfctmp = fc[NMP_A_SFCTMP * ld]; c.sfcprs = fc[NMP_A_SFCPRS * ld]; c.psfc = fc[NMP_A_PSFC * ld];
   c.uu = fc[NMP_A_UU * ld]; c.vv = fc[NMP_A_VV * ld]; c.q2 = fc[NMP_A_Q2 * ld];
-  c.soldn = fc[NMP_A_SOLDN * ld]; c.lwdn = fc[NMP_A_LWDN * ld]; c.prcp = fc[NMP_A_PRCP * ld];
+  c.soldn = fc[NMP_A_SOLDN * ld]; c.lwdn = fc[NMP_A_LWDN * ld];
   c.cosz = fc[NMP_A_COSZ * ld];
   c.status = 0;
 

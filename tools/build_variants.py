@@ -15,6 +15,7 @@ VARIANTS = {
     "outline_w2": ("-DNMP_MATH_OUTLINE", "-DNMP_WAVES_PER_EU=2"),
     "w4": ("-DNMP_WAVES_PER_EU=4",),
     "w1": ("-DNMP_WAVES_PER_EU=1",),
+    "w3": ("-DNMP_WAVES_PER_EU=3",),
     "phase": ("-DNMP_PHASE_TIMING",),
 }
 if __name__ == "__main__":
