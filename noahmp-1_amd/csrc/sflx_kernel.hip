@@ -791,6 +791,7 @@ struct Sink {
   const T* sf;        // static_f + column
   const int32_t* si;  // static_i + column
   const T* fc;        // forcing + column
+  int32_t* isnow;     // isnow + column
   // late loads: fields first needed deep in the step are read there, not at
   // kernel entry, so they do not hold registers through the energy phase
   DEV T ls(int f) const { return st[f * ld]; }
@@ -817,6 +818,7 @@ struct Sink {
     if (level == NMP_DIAG_OUT) dg[NMP_O_T2M * ld] = v;
   }
   DEV void s(int f, T v) const { st[f * ld] = v; }
+  DEV void isn(int v) const { *isnow = v; }
 };
 
 // Optional per-phase timing (build with -DNMP_PHASE_TIMING; tools only):
@@ -2117,6 +2119,19 @@ DEV void sflx_column(const DevParams& P, const KArgs<T>& A, Col<T>& c, const Sin
     for (int k = 0; k < 7; ++k)
       if (k >= kt2) c.dz[k] = -c.dz[k];
   }
+  // snow/soil temperatures, layer geometry and snow layers are final here
+  // (soilh2o/groundwater/carbon only read them): store now, free the registers
+#pragma unroll
+  for (int k = 0; k < 7; ++k) {
+    out.s(NMP_S_STC + k, c.stc[k]);
+    out.s(NMP_S_ZSNSO + k, c.zsnso[k]);
+  }
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    out.s(NMP_S_SNICE + k, c.snice[k]);
+    out.s(NMP_S_SNLIQ + k, c.snliq[k]);
+  }
+  out.isn(c.isnow);
   NMP_PHASE(11);
   // frozen ground (:4744-4752)
   if (frozen_ground) {
@@ -2648,20 +2663,11 @@ void sflx_step_kernel(const DevParams* __restrict__ gparams,
   c.cosz = fc[NMP_A_COSZ * ld];
   c.status = 0;
 
-  const Sink<T> out{a.diag ? a.diag + c0 : nullptr, a.state + c0, ld, a.diag_level, sf, si, fc};
+  const Sink<T> out{a.diag ? a.diag + c0 : nullptr, a.state + c0, ld, a.diag_level, sf, si, fc,
+                    a.isnow + c0};
   sflx_column<T, R>(sp, a, c, out);
 
   T* so = a.state + c0;
-#pragma unroll
-  for (int k = 0; k < 7; ++k) {
-    so[(NMP_S_STC + k) * ld] = c.stc[k];
-    so[(NMP_S_ZSNSO + k) * ld] = c.zsnso[k];
-  }
-#pragma unroll
-  for (int k = 0; k < 3; ++k) {
-    so[(NMP_S_SNICE + k) * ld] = c.snice[k];
-    so[(NMP_S_SNLIQ + k) * ld] = c.snliq[k];
-  }
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     so[(NMP_S_SH2O + k) * ld] = c.sh2o[k];
@@ -2676,7 +2682,6 @@ void sflx_step_kernel(const DevParams* __restrict__ gparams,
   so[NMP_S_SAI * ld] = c.sai; so[NMP_S_LFMASS * ld] = c.lfmass; so[NMP_S_RTMASS * ld] = c.rtmass;
   so[NMP_S_STMASS * ld] = c.stmass; so[NMP_S_WOOD * ld] = c.wood; so[NMP_S_STBLCP * ld] = c.stblcp;
   so[NMP_S_FASTCP * ld] = c.fastcp;
-  a.isnow[c0] = c.isnow;
   if (c.status != 0) a.status[c0] |= c.status;
 }
 
