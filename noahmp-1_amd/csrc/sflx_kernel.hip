@@ -111,10 +111,16 @@ DEV T tdfcnd(const SoilRec& S, T smc, T sh2o) {
 
 // twostream: func.f90:2215-2462 for one band / beam type
 template <class T, bool R>
-DEV void twostream(const DevParams& P, const VegRec& V, const Opt& o, int ib, int ic, T cosz,
-                   T vai, T fwet, T t, const T (&albgrd)[2], const T (&albgri)[2],
-                   const T (&rho)[2], const T (&tau)[2], T fveg, T& fab, T& fre, T& ftd, T& fti,
-                   T& gdir, T& bgap, T& wgap) {
+DEV void twostream_all(const DevParams& P, const VegRec& V, const Opt& o, T cosz, T vai, T fwet,
+                       T t, const T (&albgrd)[2], const T (&albgri)[2], const T (&rho)[2],
+                       const T (&tau)[2], T fveg, T (&fabd)[2], T (&albd)[2], T (&ftdd)[2],
+                       T (&ftid)[2], T (&fabi)[2], T (&albi)[2], T (&ftii)[2], T& gdir, T& bgap,
+                       T& wgap) {
+  // twostream (func.f90:2215-2462) for both bands x both beams.  The reference
+  // calls it 4 times; everything that does not depend on the band (crown gaps,
+  // leaf-angle geometry, the avmu/asu log factors, exp(-ext*vai)) or on the
+  // beam (h, s1, ...) is evaluated once here, with each expression's operand
+  // order unchanged, so every output is bit-identical to the 4 separate calls.
   typedef Mth<T, R> M;
   const T PAI = L(3.14159265);
   T gap = L(0.0), kopen = L(0.0);
@@ -144,82 +150,100 @@ DEV void twostream(const DevParams& P, const VegRec& V, const Opt& o, int ib, in
       kopen = L(1.0) - fveg;
     }
   }
-  T coszi = rmax(L(0.001), cosz);
+  const T coszi = rmax(L(0.001), cosz);
   T chil = rmin(rmax((T)V.xl, L(-0.4)), L(0.6));
   if (fabs(chil) <= L(0.01)) chil = L(0.01);
-  T phi1 = L(0.5) - L(0.633) * chil - L(0.330) * chil * chil;
-  T phi2 = L(0.877) * (L(1.) - L(2.) * phi1);
+  const T phi1 = L(0.5) - L(0.633) * chil - L(0.330) * chil * chil;
+  const T phi2 = L(0.877) * (L(1.) - L(2.) * phi1);
   gdir = phi1 + phi2 * coszi;
-  T ext = gdir / coszi;
-  T avmu = (L(1.) - phi1 / phi2 * M::log((phi1 + phi2) / phi1)) / phi2;
-  T omegal = rho[ib] + tau[ib];
-  T tmp0 = gdir + phi2 * coszi;
-  T tmp1 = phi1 * coszi;
-  T asu = L(0.5) * omegal * gdir / tmp0 * (L(1.) - tmp1 / tmp0 * M::log((tmp1 + tmp0) / tmp1));
-  T betadl = (L(1.) + avmu * ext) / (omegal * avmu * ext) * asu;
-  T betail = L(0.5) * (rho[ib] + tau[ib] + (rho[ib] - tau[ib]) * p2((L(1.) + chil) / L(2.))) /
-             omegal;
-  T tmp2;
-  if (t > TFRZ) {
-    tmp0 = omegal;
-    tmp1 = betadl;
-    tmp2 = betail;
-  } else {
-    T oms = (T)P.g.omegas[ib];
-    tmp0 = (L(1.0) - fwet) * omegal + fwet * oms;
-    tmp1 = ((L(1.0) - fwet) * omegal * betadl + fwet * oms * (T)P.g.betads) / tmp0;
-    tmp2 = ((L(1.0) - fwet) * omegal * betail + fwet * oms * (T)P.g.betais) / tmp0;
+  const T ext = gdir / coszi;
+  const T avmu = (L(1.) - phi1 / phi2 * M::log((phi1 + phi2) / phi1)) / phi2;
+  const T g_tmp0 = gdir + phi2 * coszi;
+  const T g_tmp1 = phi1 * coszi;
+  const T asu_f = (L(1.) - g_tmp1 / g_tmp0 * M::log((g_tmp1 + g_tmp0) / g_tmp1));
+  const T chilf = p2((L(1.) + chil) / L(2.));
+  const T s2 = M::exp(-ext * vai);
+  const T avext = avmu * ext;
+#pragma unroll
+  for (int ib = 0; ib < 2; ++ib) {
+    const T omegal = rho[ib] + tau[ib];
+    const T asu = L(0.5) * omegal * gdir / g_tmp0 * asu_f;
+    const T betadl = (L(1.) + avmu * ext) / (omegal * avmu * ext) * asu;
+    const T betail = L(0.5) * (rho[ib] + tau[ib] + (rho[ib] - tau[ib]) * chilf) / omegal;
+    T omega, betad, betai;
+    if (t > TFRZ) {
+      omega = omegal;
+      betad = betadl;
+      betai = betail;
+    } else {
+      const T oms = (T)P.g.omegas[ib];
+      omega = (L(1.0) - fwet) * omegal + fwet * oms;
+      betad = ((L(1.0) - fwet) * omegal * betadl + fwet * oms * (T)P.g.betads) / omega;
+      betai = ((L(1.0) - fwet) * omegal * betail + fwet * oms * (T)P.g.betais) / omega;
+    }
+    const T b = L(1.) - omega + omega * betai;
+    const T c = omega * betai;
+    const T tmp0 = avext;
+    const T d = tmp0 * omega * betad;
+    const T f = tmp0 * omega * (L(1.) - betad);
+    const T tmp1 = b * b - c * c;
+    const T h = M::sqrt(tmp1) / avmu;
+    T sigma = tmp0 * tmp0 - tmp1;
+    if (fabs(sigma) < L(1.e-6)) sigma = copysign(L(1.e-6), sigma);
+    const T p1 = b + avmu * h;
+    const T pp2 = b - avmu * h;
+    const T pp3 = b + tmp0;
+    const T pp4 = b - tmp0;
+    const T s1 = M::exp(-h * vai);
+#pragma unroll
+    for (int ic = 0; ic < 2; ++ic) {
+      const T alb = (ic == 0) ? albgrd[ib] : albgri[ib];
+      const T u1 = b - c / alb;
+      const T u2 = b - c * alb;
+      const T u3 = f + c * alb;
+      const T tmp2 = u1 - avmu * h;
+      const T tmp3 = u1 + avmu * h;
+      const T d1 = p1 * tmp2 / s1 - pp2 * tmp3 * s1;
+      const T tmp4 = u2 + avmu * h;
+      const T tmp5 = u2 - avmu * h;
+      const T d2 = tmp4 / s1 - tmp5 * s1;
+      T ftd, fti, fre;
+      if (ic == 0) {
+        const T h1 = -d * pp4 - c * f;
+        const T tmp6 = d - h1 * pp3 / sigma;
+        const T tmp7 = (d - c - h1 / sigma * (u1 + tmp0)) * s2;
+        const T h2 = (tmp6 * tmp2 / s1 - pp2 * tmp7) / d1;
+        const T h3 = -(tmp6 * tmp3 * s1 - p1 * tmp7) / d1;
+        const T h4 = -f * pp3 - c * d;
+        const T tmp8 = h4 / sigma;
+        const T tmp9 = (u3 - tmp8 * (u2 - tmp0)) * s2;
+        const T h5 = -(tmp8 * tmp4 / s1 + tmp9) / d2;
+        const T h6 = (tmp8 * tmp5 * s1 + tmp9) / d2;
+        ftd = s2 * (L(1.0) - gap) + gap;
+        fti = (h4 * s2 / sigma + h5 * s1 + h6 / s1) * (L(1.0) - gap);
+        fre = (h1 / sigma + h2 + h3) * (L(1.0) - gap) + albgrd[ib] * gap;
+      } else {
+        const T h7 = (c * tmp2) / (d1 * s1);
+        const T h8 = (-c * tmp3 * s1) / d1;
+        const T h9 = tmp4 / (d2 * s1);
+        const T h10 = (-tmp5 * s1) / d2;
+        ftd = L(0.);
+        fti = (h9 * s1 + h10 / s1) * (L(1.0) - kopen) + kopen;
+        fre = (h7 + h8) * (L(1.0) - kopen) + albgri[ib] * kopen;
+      }
+      const T fab = L(1.0) - fre - (L(1.0) - albgrd[ib]) * ftd - (L(1.0) - albgri[ib]) * fti;
+      if (ic == 0) {
+        fabd[ib] = fab;
+        albd[ib] = fre;
+        ftdd[ib] = ftd;
+        ftid[ib] = fti;
+      } else {
+        fabi[ib] = fab;
+        albi[ib] = fre;
+        ftii[ib] = fti;
+      }
+    }
   }
-  T omega = tmp0, betad = tmp1, betai = tmp2;
-  T b = L(1.) - omega + omega * betai;
-  T c = omega * betai;
-  tmp0 = avmu * ext;
-  T d = tmp0 * omega * betad;
-  T f = tmp0 * omega * (L(1.) - betad);
-  tmp1 = b * b - c * c;
-  T h = M::sqrt(tmp1) / avmu;
-  T sigma = tmp0 * tmp0 - tmp1;
-  if (fabs(sigma) < L(1.e-6)) sigma = copysign(L(1.e-6), sigma);
-  T p1 = b + avmu * h;
-  T pp2 = b - avmu * h;
-  T pp3 = b + tmp0;
-  T pp4 = b - tmp0;
-  T s1 = M::exp(-h * vai);
-  T s2 = M::exp(-ext * vai);
-  T alb = (ic == 0) ? albgrd[ib] : albgri[ib];
-  T u1 = b - c / alb;
-  T u2 = b - c * alb;
-  T u3 = f + c * alb;
-  tmp2 = u1 - avmu * h;
-  T tmp3 = u1 + avmu * h;
-  T d1 = p1 * tmp2 / s1 - pp2 * tmp3 * s1;
-  T tmp4 = u2 + avmu * h;
-  T tmp5 = u2 - avmu * h;
-  T d2 = tmp4 / s1 - tmp5 * s1;
-  T h1 = -d * pp4 - c * f;
-  T tmp6 = d - h1 * pp3 / sigma;
-  T tmp7 = (d - c - h1 / sigma * (u1 + tmp0)) * s2;
-  T h2 = (tmp6 * tmp2 / s1 - pp2 * tmp7) / d1;
-  T h3 = -(tmp6 * tmp3 * s1 - p1 * tmp7) / d1;
-  T h4 = -f * pp3 - c * d;
-  T tmp8 = h4 / sigma;
-  T tmp9 = (u3 - tmp8 * (u2 - tmp0)) * s2;
-  T h5 = -(tmp8 * tmp4 / s1 + tmp9) / d2;
-  T h6 = (tmp8 * tmp5 * s1 + tmp9) / d2;
-  T h7 = (c * tmp2) / (d1 * s1);
-  T h8 = (-c * tmp3 * s1) / d1;
-  T h9 = tmp4 / (d2 * s1);
-  T h10 = (-tmp5 * s1) / d2;
-  if (ic == 0) {
-    ftd = s2 * (L(1.0) - gap) + gap;
-    fti = (h4 * s2 / sigma + h5 * s1 + h6 / s1) * (L(1.0) - gap);
-    fre = (h1 / sigma + h2 + h3) * (L(1.0) - gap) + albgrd[ib] * gap;
-  } else {
-    ftd = L(0.);
-    fti = (h9 * s1 + h10 / s1) * (L(1.0) - kopen) + kopen;
-    fre = (h7 + h8) * (L(1.0) - kopen) + albgri[ib] * kopen;
-  }
-  fab = L(1.0) - fre - (L(1.0) - albgrd[ib]) * ftd - (L(1.0) - albgri[ib]) * fti;
 }
 
 // sfcdif1: func.f90:3353-3508
@@ -989,6 +1013,10 @@ DEV void sflx_column(const DevParams& P, const KArgs<T>& A, Col<T>& c, const Sin
   T ftdd[2] = {L(0.), L(0.)}, ftid[2] = {L(0.), L(0.)}, ftii[2] = {L(0.), L(0.)};
   T fsun = L(0.0);
   if (c.cosz > L(0.0)) {
+    // snow-age / albedo state is only read and updated in daylight (:1823):
+    // load it here, store it at the end of this block
+    c.albold = out.ls(NMP_S_ALBOLD); c.tauss = out.ls(NMP_S_TAUSS);
+    c.qsnow = out.ls(NMP_S_QSNOW); c.sneqvo = out.ls(NMP_S_SNEQVO);
     const T mpe6 = L(1.0E-06);
     T rho[2], tau[2];
     T vaia = elai + esai;
@@ -1059,18 +1087,14 @@ DEV void sflx_column(const DevParams& P, const KArgs<T>& A, Col<T>& c, const Sin
       albgri[ib] = albsoi * (L(1.0) - fsno) + albsni[ib] * fsno;
     }
     T gdir = L(0.0);
-#pragma unroll
-    for (int ib = 0; ib < 2; ++ib) {
-      twostream<T, R>(P, V, o, ib, 0, c.cosz, vaia, c.fwet, c.tv, albgrd, albgri, rho, tau, fveg,
-                      fabd[ib], albd[ib], ftdd[ib], ftid[ib], gdir, bgap, wgap);
-      T ftdi_unused;
-      twostream<T, R>(P, V, o, ib, 1, c.cosz, vaia, c.fwet, c.tv, albgrd, albgri, rho, tau, fveg,
-                      fabi[ib], albi[ib], ftdi_unused, ftii[ib], gdir, bgap, wgap);
-    }
+    twostream_all<T, R>(P, V, o, c.cosz, vaia, c.fwet, c.tv, albgrd, albgri, rho, tau, fveg, fabd,
+                        albd, ftdd, ftid, fabi, albi, ftii, gdir, bgap, wgap);
     T ext = gdir / c.cosz * M::sqrt(L(1.0) - rho[0] - tau[0]);
     fsun = (L(1.0) - M::exp(-ext * vaia)) / rmax(ext * vaia, mpe6);
     ext = fsun;
     fsun = (ext < L(0.01)) ? L(0.) : ext;
+    out.s(NMP_S_ALBOLD, c.albold);
+    out.s(NMP_S_TAUSS, c.tauss);
   }
   T fsha = L(1.0) - fsun;
   T laisun = elai * fsun;
@@ -1112,8 +1136,6 @@ DEV void sflx_column(const DevParams& P, const KArgs<T>& A, Col<T>& c, const Sin
   out.template d<NMP_D_FVEG>(fveg);
   out.template d<NMP_D_BGAP>(bgap);
   out.template d<NMP_D_WGAP>(wgap);
-  out.s(NMP_S_ALBOLD, c.albold);
-  out.s(NMP_S_TAUSS, c.tauss);
   T emv = L(1.0) - M::exp(-(elai + esai) / L(1.0));
   T emg;
   if (c.ice == 1)
@@ -2645,9 +2667,11 @@ void sflx_step_kernel(const DevParams* __restrict__ gparams,
   }
   c.tv = st[NMP_S_TV * ld]; c.tg = st[NMP_S_TG * ld];
   c.fwet = st[NMP_S_FWET * ld]; c.snowh = st[NMP_S_SNOWH * ld];
-  c.sneqv = st[NMP_S_SNEQV * ld]; c.sneqvo = st[NMP_S_SNEQVO * ld];
-  c.albold = st[NMP_S_ALBOLD * ld]; c.tauss = st[NMP_S_TAUSS * ld];
-  c.qsnow = st[NMP_S_QSNOW * ld]; c.lai = st[NMP_S_LAI * ld]; c.sai = st[NMP_S_SAI * ld];
+  c.sneqv = st[NMP_S_SNEQV * ld];
+  c.lai = st[NMP_S_LAI * ld]; c.sai = st[NMP_S_SAI * ld];
+  // ALBOLD/TAUSS/QSNOW/SNEQVO: loaded where used (daylight radiation block);
+  // QSNOW and SNEQVO are reassigned before the water phase reads them
+  c.albold = c.tauss = c.qsnow = c.sneqvo = (T)0;
   c.isnow = a.isnow[c0];
   const T* sf = a.static_f + c0;
   c.lat = sf[NMP_F_LAT * ld]; c.zref = sf[NMP_F_ZLVL * ld]; c.shdfac = sf[NMP_F_SHDFAC * ld];
