@@ -9,6 +9,7 @@
 #pragma once
 #include <stdint.h>
 
+#include "glibc_math.h"
 #include "noahmp_engine.h"
 
 namespace nmp {
@@ -26,23 +27,32 @@ struct VegRec {  // one USGS/MODIS vegetation type (veg_param.f90:19-74)
 
 struct SoilRec {  // one soil type (soil_param.f90:13-23)
   float bexp, smcmax, smcref, smcwlt, psisat, dksat, dwsat, quartz, kdt, frzx;
+  // soil-type-only factors of tdfcnd (func.f90:1552-1593), evaluated once on
+  // the host with the glibc-exact libm: THKS**(1-SMCMAX) and THKDRY
+  float tdf_thks_pow, tdf_thkdry;
 };
 
 struct GenRec {  // GENPARMMP.TBL scalars + soil colours (gen_param.f90:12-48, soil_param.f90:27-28)
   float slope[NMP_MSLOPETYP];
   float csoil, zbot, czil, timean, fsatmax, mltfct, z0sno, ssi, swemax;
+  float exp_mtimean;  // EXP(-TIMEAN) (groundwater :6531, zwteq), glibc-exact
   float alblake[2], omegas[2], betads, betais, emssoil, emslake;
   float albsat[NMP_MSLCOL][2], albdry[NMP_MSLCOL][2];
   int32_t isurban, iswater, isbarren, isice, isegblf, pad_;
 };
 
-struct DevParams {
+// alignas(16): the kernel stages the struct into LDS with int4 copies of
+// sizeof/16 chunks, so the size must be a whole number of 16-byte chunks
+// (9400 B before this alignment left the last 8 bytes -- veg[26].nroot/c3c4 --
+// unstaged).
+struct alignas(16) DevParams {
   GenRec g;
   SoilRec soil[NMP_MSLTYP];
   VegRec veg[NMP_MLUTYP];
 };
 
-static_assert(sizeof(DevParams) % 16 == 0 || true, "");
+// host copy of the glibc libm tables (glibc_math.h), for host-side precompute
+inline const gm::GmTables kHostGmTables = {GM_EXP2F_TAB, GM_LOGF_TAB, GM_POWF_TAB};
 
 inline void pack_dev_params(const nmp_params& p, DevParams& d) {
   for (int i = 0; i < NMP_MSLOPETYP; ++i) d.g.slope[i] = p.slope[i];
@@ -66,7 +76,15 @@ inline void pack_dev_params(const nmp_params& p, DevParams& d) {
     r.bexp = p.bexp[s]; r.smcmax = p.smcmax[s]; r.smcref = p.smcref[s]; r.smcwlt = p.smcwlt[s];
     r.psisat = p.psisat[s]; r.dksat = p.dksat[s]; r.dwsat = p.dwsat[s]; r.quartz = p.quartz[s];
     r.kdt = p.kdt[s]; r.frzx = p.frzx[s];
+    // tdfcnd: THKS = THKQTZ**QZ * 2.0**(1-QZ); THKSAT's first factor THKS**(1-SMCMAX);
+    // GAMMD = (1-SMCMAX)*2700; THKDRY = (0.135*GAMMD + 64.7) / (2700 - 0.947*GAMMD)
+    const gm::GmTables& T = kHostGmTables;
+    const float thks = gm::powf(7.7f, r.quartz, T) * gm::exp2f(1.0f - r.quartz, T);
+    r.tdf_thks_pow = gm::powf(thks, 1.0f - r.smcmax, T);
+    const float gammd = (1.0f - r.smcmax) * 2700.0f;
+    r.tdf_thkdry = (0.135f * gammd + 64.7f) / (2700.0f - 0.947f * gammd);
   }
+  d.g.exp_mtimean = gm::expf(-p.timean, kHostGmTables);
   for (int v = 0; v < NMP_MLUTYP; ++v) {
     VegRec& r = d.veg[v];
     r.xl = p.xl[v];
@@ -93,3 +111,5 @@ inline void pack_dev_params(const nmp_params& p, DevParams& d) {
 }
 
 }  // namespace nmp
+
+static_assert(sizeof(nmp::DevParams) % 16 == 0, "DevParams is staged to LDS with int4 copies");

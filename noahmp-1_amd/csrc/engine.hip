@@ -57,6 +57,10 @@ void fill_args(nmp::KArgs<T>& a, const nmp_engine* e, int64_t ncol, int64_t ld,
   a.julian = julian;
   a.yearlen = yearlen;
   a.diag_level = diag_level;
+  // launch-uniform transcendentals of the fp32 "ref" path, evaluated once on the
+  // host with the same glibc-exact code the kernel runs (csrc/glibc_math.h)
+  a.c_exp_m4 = gm::expf(-4.0f, nmp::kHostGmTables);                 // soilh2o FCR :5900-5904
+  a.c_albdecay = gm::expf(-0.01f * dt / 3600.0f, nmp::kHostGmTables);  // snowalb_class :2130
   const nmp_options& o = e->opts;
   a.o = nmp::Opt{o.opt_veg, o.opt_crs, o.opt_btr, o.opt_run, o.opt_sfc, o.opt_frz,
                  o.opt_inf, o.opt_rad, o.opt_alb, o.opt_snf, o.opt_tbot, o.opt_stc};
@@ -116,7 +120,7 @@ int nmp_init(const nmp_params* params, const nmp_options* opts, int device, int 
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) return NMP_E_DEVICE;
   if (ensure_device(device) != NMP_OK) return NMP_E_DEVICE;
-  nmp::DevParams host;
+  nmp::DevParams host{};
   std::memset(&host, 0, sizeof(host));
   nmp::pack_dev_params(*params, host);
   nmp::DevParams* d = nullptr;

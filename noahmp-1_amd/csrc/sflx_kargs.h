@@ -19,6 +19,7 @@ struct KArgs {
   float dt, julian;
   int yearlen;
   int diag_level;
+  float c_exp_m4, c_albdecay;  // host-precomputed EXP(-4.0), EXP(-0.01*DT/3600) (fp32 ref)
   Opt o;
   T* state;
   int32_t* isnow;

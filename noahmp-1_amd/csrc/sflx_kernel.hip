@@ -95,12 +95,19 @@ DEV T tdfcnd(const SoilRec& S, T smc, T sh2o) {
   T satratio = smc / smcmax;
   T thkw = L(0.57);
   T thkqtz = L(7.7);
-  T thks = M::pow(thkqtz, quartz) * M::exp2(L(1.0) - quartz);  // 2.0**x -> exp2
   T xunfroz = sh2o / smc;
   T xu = xunfroz * smcmax;
-  T thksat = M::pow(thks, L(1.0) - smcmax) * M::pow(TKICE, smcmax - xu) * M::pow(thkw, xu);
-  T gammd = (L(1.0) - smcmax) * L(2700.0);
-  T thkdry = (L(0.135) * gammd + L(64.7)) / (L(2700.0) - L(0.947) * gammd);
+  T thksat, thkdry;
+  if constexpr (sizeof(T) == 4 && R) {
+    // soil-type-only factors precomputed on the host (dev_params.h), bit-identical
+    thksat = (T)S.tdf_thks_pow * M::pow(TKICE, smcmax - xu) * M::pow(thkw, xu);
+    thkdry = (T)S.tdf_thkdry;
+  } else {
+    T thks = M::pow(thkqtz, quartz) * M::exp2(L(1.0) - quartz);  // 2.0**x -> exp2
+    thksat = M::pow(thks, L(1.0) - smcmax) * M::pow(TKICE, smcmax - xu) * M::pow(thkw, xu);
+    T gammd = (L(1.0) - smcmax) * L(2700.0);
+    thkdry = (L(0.135) * gammd + L(64.7)) / (L(2700.0) - L(0.947) * gammd);
+  }
   T ake;
   if ((sh2o + L(0.0005)) < smc)
     ake = satratio;
@@ -1058,7 +1065,8 @@ DEV void sflx_column(const DevParams& P, const KArgs<T>& A, Col<T>& c, const Sin
       albsnd[1] = albsni[1] + L(0.4) * fzen * (L(1.0) - albsni[1]);
     }
     if (o.alb == 2) {  // snowalb_class: func.f90:2105-2151
-      T alb = L(0.55) + (c.albold - L(0.55)) * M::exp(-L(0.01) * DT / L(3600.0));
+      const T decay = (sizeof(T) == 4 && R) ? (T)A.c_albdecay : M::exp(-L(0.01) * DT / L(3600.0));
+      T alb = L(0.55) + (c.albold - L(0.55)) * decay;
       if (c.qsnow > L(0.0))
         alb = alb + rmin(c.qsnow * DT, (T)P.g.swemax) * (L(0.84) - alb) / (T)P.g.swemax;
       albsnd[0] = albsnd[1] = albsni[0] = albsni[1] = alb;
@@ -2195,8 +2203,8 @@ DEV void sflx_column(const DevParams& P, const KArgs<T>& A, Col<T>& c, const Sin
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       T fice = rmin(L(1.0), c.sice[k] / smcmax);
-      fcr[k] = rmax(L(0.0), M::exp(-L(4.0) * (L(1.0) - fice)) - M::exp(-L(4.0))) /
-               (L(1.0) - M::exp(-L(4.0)));
+      const T e4 = (sizeof(T) == 4 && R) ? (T)A.c_exp_m4 : M::exp(-L(4.0));
+      fcr[k] = rmax(L(0.0), M::exp(-L(4.0) * (L(1.0) - fice)) - e4) / (L(1.0) - e4);
     }
     T sicemax = L(0.0);
 #pragma unroll
@@ -2221,7 +2229,7 @@ DEV void sflx_column(const DevParams& P, const KArgs<T>& A, Col<T>& c, const Sin
           break;
         }
       }
-      runsub = (L(1.0) - fcrmax) * L(4.0) * M::exp(-(T)P.g.timean) * M::exp(-L(2.0) * c.zwt);
+      runsub = (L(1.0) - fcrmax) * L(4.0) * ((sizeof(T) == 4 && R) ? (T)P.g.exp_mtimean : M::exp(-(T)P.g.timean)) * M::exp(-L(2.0) * c.zwt);
     }
     if (c.lutyp == P.g.isurban) fcr[0] = L(0.95);
     if (o.run == 1 || o.run == 2) {
@@ -2453,7 +2461,7 @@ DEV void sflx_column(const DevParams& P, const KArgs<T>& A, Col<T>& c, const Sin
         iwt = 1;
       else if (c.zwt <= -zsoil[3])
         iwt = 2;
-      T qdis = (L(1.0) - fcrmax) * L(5.0) * M::exp(-(T)P.g.timean) * M::exp(-L(6.0) * (c.zwt - L(2.0)));
+      T qdis = (L(1.0) - fcrmax) * L(5.0) * ((sizeof(T) == 4 && R) ? (T)P.g.exp_mtimean : M::exp(-(T)P.g.timean)) * M::exp(-L(6.0) * (c.zwt - L(2.0)));
       // S_NODE is real(8) in the reference (:6501): evaluate the matric potential in fp64
       double s_node = (double)rmin(L(1.0), dget(smcg, iwt) / smcmax);
       s_node = fmax(s_node, (double)0.01f);
