@@ -23,6 +23,10 @@ struct VegRec {  // one USGS/MODIS vegetation type (veg_param.f90:19-74)
   float kc25, akc, ko25, ako, vcmx25, avcmx, bp, mp, qe25, folnmx, tmin;
   float rmf25, rms25, rmr25, arm, mrp;
   int32_t nroot, c3c4;
+  // veg-type-only transcendentals, evaluated once on the host (glibc-exact):
+  // twostream AVMU (:2338-2341), LOG(HVT/Z0MVT) (vege_flux UC :2725) and
+  // LOG((2+Z0M)/Z0M) (sfcdif1 TMPCM2 :3419 with Z0M = Z0MVT)
+  float avmu, log_hvt_z0m, log_2z0m;
 };
 
 struct SoilRec {  // one soil type (soil_param.f90:13-23)
@@ -30,6 +34,7 @@ struct SoilRec {  // one soil type (soil_param.f90:13-23)
   // soil-type-only factors of tdfcnd (func.f90:1552-1593), evaluated once on
   // the host with the glibc-exact libm: THKS**(1-SMCMAX) and THKDRY
   float tdf_thks_pow, tdf_thkdry;
+  float rsurf_den;  // 2.2E-5*SMCMAX**2*(1-SMCWLT/SMCMAX)**(2+3/BEXP) (rsurf :1150-1151)
 };
 
 struct GenRec {  // GENPARMMP.TBL scalars + soil colours (gen_param.f90:12-48, soil_param.f90:27-28)
@@ -83,6 +88,8 @@ inline void pack_dev_params(const nmp_params& p, DevParams& d) {
     r.tdf_thks_pow = gm::powf(thks, 1.0f - r.smcmax, T);
     const float gammd = (1.0f - r.smcmax) * 2700.0f;
     r.tdf_thkdry = (0.135f * gammd + 64.7f) / (2700.0f - 0.947f * gammd);
+    r.rsurf_den = 2.2E-5f * r.smcmax * r.smcmax *
+                  gm::powf(1.0f - r.smcwlt / r.smcmax, 2.0f + 3.0f / r.bexp, T);
   }
   d.g.exp_mtimean = gm::expf(-p.timean, kHostGmTables);
   for (int v = 0; v < NMP_MLUTYP; ++v) {
@@ -107,6 +114,17 @@ inline void pack_dev_params(const nmp_params& p, DevParams& d) {
     r.rmf25 = p.rmf25[v]; r.rms25 = p.rms25[v]; r.rmr25 = p.rmr25[v]; r.arm = p.arm[v];
     r.mrp = p.mrp[v];
     r.nroot = p.nroot[v]; r.c3c4 = p.c3c4[v];
+    {
+      const gm::GmTables& T = kHostGmTables;
+      float chil = r.xl > -0.4f ? r.xl : -0.4f;  // rmin(rmax(XL,-0.4),0.6) as the kernel
+      chil = chil < 0.6f ? chil : 0.6f;
+      if (__builtin_fabsf(chil) <= 0.01f) chil = 0.01f;
+      const float phi1 = 0.5f - 0.633f * chil - 0.330f * chil * chil;
+      const float phi2 = 0.877f * (1.0f - 2.0f * phi1);
+      r.avmu = (1.0f - phi1 / phi2 * gm::logf((phi1 + phi2) / phi1, T)) / phi2;
+      r.log_hvt_z0m = gm::logf(r.hvt / r.z0mvt, T);
+      r.log_2z0m = gm::logf((2.0f + r.z0mvt) / r.z0mvt, T);
+    }
   }
 }
 

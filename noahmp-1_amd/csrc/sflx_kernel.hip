@@ -164,7 +164,8 @@ DEV void twostream_all(const DevParams& P, const VegRec& V, const Opt& o, T cosz
   const T phi2 = L(0.877) * (L(1.) - L(2.) * phi1);
   gdir = phi1 + phi2 * coszi;
   const T ext = gdir / coszi;
-  const T avmu = (L(1.) - phi1 / phi2 * M::log((phi1 + phi2) / phi1)) / phi2;
+  const T avmu = (sizeof(T) == 4 && R) ? (T)V.avmu  // veg-type-only (dev_params.h)
+                                       : (L(1.) - phi1 / phi2 * M::log((phi1 + phi2) / phi1)) / phi2;
   const T g_tmp0 = gdir + phi2 * coszi;
   const T g_tmp1 = phi1 * coszi;
   const T asu_f = (L(1.) - g_tmp1 / g_tmp0 * M::log((g_tmp1 + g_tmp0) / g_tmp1));
@@ -261,12 +262,12 @@ template <class T, bool R>
 struct Sfc1Logs {
   T tmpcm, tmpch, tmpcm2, tmpch2;
   DEV Sfc1Logs() : tmpcm(0), tmpch(0), tmpcm2(0), tmpch2(0) {}
-  DEV Sfc1Logs(T zlvl, T zpd, T z0m, T z0h, int& status) {
+  DEV Sfc1Logs(T zlvl, T zpd, T z0m, T z0h, int& status, const T* log_2z0m = nullptr) {
     typedef Mth<T, R> M;
     if (zlvl <= zpd) status |= NMP_ST_ZLVL;  // :3412-3415
     tmpcm = M::log((zlvl - zpd) / z0m);
     tmpch = (z0h == z0m) ? tmpcm : M::log((zlvl - zpd) / z0h);
-    tmpcm2 = M::log((L(2.0) + z0m) / z0m);
+    tmpcm2 = log_2z0m ? *log_2z0m : M::log((L(2.0) + z0m) / z0m);
     tmpch2 = (z0h == z0m) ? tmpcm2 : M::log((L(2.0) + z0h) / z0h);
   }
 };
@@ -931,6 +932,10 @@ DEV void sflx_column(const DevParams& P, const KArgs<T>& A, Col<T>& c, const Sin
     c.lai = L(0.0);
     c.sai = L(0.0);
   }
+  if (!(o.veg == 2 || o.veg == 5)) {  // no carbon model: LAI/SAI are final here
+    out.s(NMP_S_LAI, c.lai);
+    out.s(NMP_S_SAI, c.sai);
+  }
   T elai, esai, igs, htop;
   {
     T hvt = (T)V.hvt, hvb = (T)V.hvb;
@@ -1190,8 +1195,9 @@ DEV void sflx_column(const DevParams& P, const KArgs<T>& A, Col<T>& c, const Sin
   } else {
     T l_rsurf = (-zsoil[0]) * (M::exp(p5(L(1.0) - rmin(L(1.0), c.sh2o[0] / smcmax))) - L(1.0)) /
                 (L(2.71828) - L(1.0));
-    T d_rsurf = L(2.2E-5) * smcmax * smcmax *
-                M::pow(L(1.0) - smcwlt / smcmax, L(2.0) + L(3.0) / bexp);
+    T d_rsurf = (sizeof(T) == 4 && R) ? (T)S.rsurf_den  // soil-type-only (dev_params.h)
+                                      : L(2.2E-5) * smcmax * smcmax *
+                                            M::pow(L(1.0) - smcwlt / smcmax, L(2.0) + L(3.0) / bexp);
     rsurf = l_rsurf / d_rsurf;
     if (c.sh2o[0] < L(0.01) && c.snowh == L(0.0)) rsurf = L(1.0E6);
     T psi = -psisat * M::pow(rmax(L(0.01), c.sh2o[0]) / smcmax, -bexp);
@@ -1234,15 +1240,19 @@ DEV void sflx_column(const DevParams& P, const KArgs<T>& A, Col<T>& c, const Sin
     T estg = (tt > L(0.0)) ? esatw : esati;
     c.qsfc = L(0.622) * eair / (c.psfc - L(0.378) * eair);
     T hcan = htop;
-    T uc = ur * M::log(hcan / z0m) / M::log(zlvl / z0m);
+    // HCAN = HVT and Z0M = Z0MVT here: LOG(HCAN/Z0M) is veg-type-only
+    T uc = ur * ((sizeof(T) == 4 && R) ? (T)V.log_hvt_z0m : M::log(hcan / z0m)) / M::log(zlvl / z0m);
     if ((hcan - zpd) <= L(0.0)) c.status |= NMP_ST_HCAN;
     T air = -emv * (L(1.0) + (L(1.0) - emv) * (L(1.0) - emg)) * c.lwdn -
             emv * emg * SB * p4(tgv);
     T cir = (L(2.0) - emv * (L(1.0) - emg)) * emv * SB;
     T rahc = L(1.0);
     const T sqrt_dleaf_uc = M::sqrt((T)V.dleaf / uc);  // ragrb :3349, loop-invariant
-    const Sfc1Logs<T, R> lgv = (o.sfc == 1) ? Sfc1Logs<T, R>(zlvl, zpd, z0m, z0h, c.status)
-                                            : Sfc1Logs<T, R>{};
+    const T log_2z0m_v = (T)V.log_2z0m;  // Z0M = Z0MVT: veg-type-only
+    const Sfc1Logs<T, R> lgv =
+        (o.sfc == 1) ? Sfc1Logs<T, R>(zlvl, zpd, z0m, z0h, c.status,
+                                      (sizeof(T) == 4 && R) ? &log_2z0m_v : nullptr)
+                     : Sfc1Logs<T, R>{};
 #pragma unroll 1
     for (int iter = 1; iter <= 20; ++iter) {
       if (o.sfc == 1)
@@ -1347,7 +1357,7 @@ DEV void sflx_column(const DevParams& P, const KArgs<T>& A, Col<T>& c, const Sin
       ghv = sag - (irg + shg + evg);
     }
     if (o.sfc == 1 || o.sfc == 2) {
-      chv2 = fv * KARMAN / (M::log((L(2.0) + z0h) / z0h) - fh2);
+      chv2 = fv * KARMAN / (((o.sfc == 1) ? lgv.tmpch2 : M::log((L(2.0) + z0h) / z0h)) - fh2);
       if (chv2 < L(1.E-5)) {
         t2mv = c.tah;
         q2v = c.qsfc;
@@ -1426,7 +1436,7 @@ DEV void sflx_column(const DevParams& P, const KArgs<T>& A, Col<T>& c, const Sin
       ghb = sag - (irb + shb + evb);
     }
     if (o.sfc == 1 || o.sfc == 2) {
-      chb2 = fv * KARMAN / (M::log((L(2.0) + z0h) / z0h) - fh2);
+      chb2 = fv * KARMAN / (((o.sfc == 1) ? lgb.tmpch2 : M::log((L(2.0) + z0h) / z0h)) - fh2);
       if (chb2 < L(1.0E-5)) {
         t2mb = tgb;
         q2b = c.qsfc;
@@ -1844,9 +1854,7 @@ DEV void sflx_column(const DevParams& P, const KArgs<T>& A, Col<T>& c, const Sin
   const T qprecc = L(0.10) * prcp_w;  // atm :517-518
   const T qprecl = L(0.90) * prcp_w;
   c.zwt = out.ls(NMP_S_ZWT); c.wa = out.ls(NMP_S_WA); c.wt = out.ls(NMP_S_WT);
-  c.wslake = out.ls(NMP_S_WSLAKE); c.lfmass = out.ls(NMP_S_LFMASS);
-  c.rtmass = out.ls(NMP_S_RTMASS); c.stmass = out.ls(NMP_S_STMASS); c.wood = out.ls(NMP_S_WOOD);
-  c.stblcp = out.ls(NMP_S_STBLCP); c.fastcp = out.ls(NMP_S_FASTCP);
+  c.wslake = out.ls(NMP_S_WSLAKE);
   c.slptyp = out.li(NMP_I_SLOPETYP);
   T ecan, etran, runsrf = L(0.0), runsub = L(0.0), qsnbot = L(0.0), ponding1 = L(0.0);
   T ponding2 = L(0.0), fpice = L(0.0), snoflow = L(0.0);
@@ -1941,6 +1949,9 @@ DEV void sflx_column(const DevParams& P, const KArgs<T>& A, Col<T>& c, const Sin
       snowhin = L(0.0);
     }
   }
+  // canopy water / temperature are final after canwater
+  out.s(NMP_S_CANLIQ, c.canliq); out.s(NMP_S_CANICE, c.canice);
+  out.s(NMP_S_FWET, c.fwet); out.s(NMP_S_TV, c.tv); out.s(NMP_S_QSNOW, c.qsnow);
   out.template d<NMP_D_ECAN>(ecan);
   out.template d<NMP_D_ETRAN>(etran);
   out.template d<NMP_D_FPICE>(fpice);
@@ -2520,6 +2531,14 @@ DEV void sflx_column(const DevParams& P, const KArgs<T>& A, Col<T>& c, const Sin
   }
   runsub = runsub + snoflow;
   // ===================== end water =====================
+  // soil water and aquifer are final after the water phase (carbon only reads SMC)
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    out.s(NMP_S_SH2O + k, c.sh2o[k]);
+    out.s(NMP_S_SMC + k, c.smc[k]);
+  }
+  out.s(NMP_S_ZWT, c.zwt); out.s(NMP_S_WA, c.wa); out.s(NMP_S_WT, c.wt);
+  out.s(NMP_S_WSLAKE, c.wslake);
   out.template d<NMP_D_RUNSRF>(runsrf);
   out.template d<NMP_D_RUNSUB>(runsub);
   out.template d<NMP_D_QSNBOT>(qsnbot);
@@ -2530,6 +2549,10 @@ DEV void sflx_column(const DevParams& P, const KArgs<T>& A, Col<T>& c, const Sin
   // carbon + co2flux (opt_veg 2|5): func.f90:6642-7025
   T gpp = L(0.0), npp = L(0.0), nee = L(0.0);
   if (o.veg == 2 || o.veg == 5) {
+    // carbon pools are read and written only when the carbon model runs
+    c.lfmass = out.ls(NMP_S_LFMASS); c.rtmass = out.ls(NMP_S_RTMASS);
+    c.stmass = out.ls(NMP_S_STMASS); c.wood = out.ls(NMP_S_WOOD);
+    c.stblcp = out.ls(NMP_S_STBLCP); c.fastcp = out.ls(NMP_S_FASTCP);
     if (c.lutyp == P.g.iswater || c.lutyp == P.g.isbarren || c.lutyp == P.g.isice ||
         c.lutyp == P.g.isurban) {
       c.lai = c.sai = L(0.0);
@@ -2614,6 +2637,10 @@ DEV void sflx_column(const DevParams& P, const KArgs<T>& A, Col<T>& c, const Sin
       c.lai = rmax(c.lfmass * lapm, LAIMIN);
       c.sai = rmax(c.stmass * sapm, XSAMIN);
     }
+    out.s(NMP_S_LAI, c.lai); out.s(NMP_S_SAI, c.sai);
+    out.s(NMP_S_LFMASS, c.lfmass); out.s(NMP_S_RTMASS, c.rtmass);
+    out.s(NMP_S_STMASS, c.stmass); out.s(NMP_S_WOOD, c.wood);
+    out.s(NMP_S_STBLCP, c.stblcp); out.s(NMP_S_FASTCP, c.fastcp);
   }
 
   out.template d<NMP_D_NEE>(nee);
@@ -2630,6 +2657,7 @@ DEV void sflx_column(const DevParams& P, const KArgs<T>& A, Col<T>& c, const Sin
     c.sneqv = L(0.0);
   }
   out.template d<NMP_D_Q2B>(q2b);
+  out.s(NMP_S_QSFC, c.qsfc); out.s(NMP_S_SNOWH, c.snowh); out.s(NMP_S_SNEQV, c.sneqv);
   NMP_PHASE(15);
 }
 
@@ -2699,21 +2727,6 @@ void sflx_step_kernel(const DevParams* __restrict__ gparams,
                     a.isnow + c0};
   sflx_column<T, R>(sp, a, c, out);
 
-  T* so = a.state + c0;
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    so[(NMP_S_SH2O + k) * ld] = c.sh2o[k];
-    so[(NMP_S_SMC + k) * ld] = c.smc[k];
-  }
-  so[NMP_S_TV * ld] = c.tv;
-  so[NMP_S_FWET * ld] = c.fwet; so[NMP_S_CANLIQ * ld] = c.canliq;
-  so[NMP_S_CANICE * ld] = c.canice; so[NMP_S_QSFC * ld] = c.qsfc; so[NMP_S_SNOWH * ld] = c.snowh;
-  so[NMP_S_SNEQV * ld] = c.sneqv;
-  so[NMP_S_QSNOW * ld] = c.qsnow; so[NMP_S_ZWT * ld] = c.zwt; so[NMP_S_WA * ld] = c.wa;
-  so[NMP_S_WT * ld] = c.wt; so[NMP_S_WSLAKE * ld] = c.wslake; so[NMP_S_LAI * ld] = c.lai;
-  so[NMP_S_SAI * ld] = c.sai; so[NMP_S_LFMASS * ld] = c.lfmass; so[NMP_S_RTMASS * ld] = c.rtmass;
-  so[NMP_S_STMASS * ld] = c.stmass; so[NMP_S_WOOD * ld] = c.wood; so[NMP_S_STBLCP * ld] = c.stblcp;
-  so[NMP_S_FASTCP * ld] = c.fastcp;
   if (c.status != 0) a.status[c0] |= c.status;
 }
 
