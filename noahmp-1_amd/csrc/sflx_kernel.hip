@@ -2668,7 +2668,10 @@ template <class T, bool R>
 #ifndef NMP_WAVES_PER_EU
 #define NMP_WAVES_PER_EU 3
 #endif
-__global__ __launch_bounds__(256)
+#ifndef NMP_BLOCK
+#define NMP_BLOCK 256
+#endif
+__global__ __launch_bounds__(NMP_BLOCK)
 __attribute__((amdgpu_waves_per_eu(sizeof(T) == 4 ? NMP_WAVES_PER_EU : 1)))
 void sflx_step_kernel(const DevParams* __restrict__ gparams,
                                                           KArgs<T> a) {
@@ -2733,7 +2736,7 @@ void sflx_step_kernel(const DevParams* __restrict__ gparams,
 // launch wrapper (one instantiation per precision / math policy)
 template <class T, bool R>
 hipError_t launch_sflx(const DevParams* dparams, const KArgs<T>& a, hipStream_t stream) {
-  const int block = 256;
+  const int block = NMP_BLOCK;
   const int64_t grid = (a.ncol + block - 1) / block;
   if (grid == 0) return hipSuccess;
   hipLaunchKernelGGL((sflx_step_kernel<T, R>), dim3((unsigned)grid), dim3(block), 0, stream,

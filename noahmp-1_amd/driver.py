@@ -1,0 +1,128 @@
+"""Offline driver: the time loop behind run/main.py.
+
+The reference's driver parses the namelist and stops (run/main.py:12-14;
+offline/noahmp_config.py has no time loop, forcing reader or writer, SURVEY
+8f).  `OfflineDriver` is that missing loop around the engine:
+
+* steps begdatetime -> enddatetime by `timestep` (Config), calling
+  `Engine.step` for every column each step; JULIAN / YEARLEN / COSZ are
+  computed per step at the step's start time (timeman.py);
+* forcing comes from a provider `forcing(step, t) -> (12, n)` array; the
+  reference's LDASIN files are not in the repository, so `SyntheticForcing`
+  (the seeded diurnal generator the tests and bench use) is the default;
+* output steps (Config.output_frequency) write the 16 surface fluxes as
+  ``<outdir>/<YYYYMMDDHH>.LDASOUT.npz``;
+* restart steps (Config.restart_frequency, calendar months allowed) write the
+  complete SoA state as ``<resdir>/RESTART.<YYYYMMDDHH>.npz``, which
+  `load_restart` reads back -- the state SoA *is* the restart.
+
+Multi-rank: each rank drives its own column shard; at output steps the
+diagnostics are all-gathered (shard.gather_diag) and rank 0 writes them.
+"""
+from __future__ import annotations
+
+import datetime
+import os
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from . import cases, layout as L, shard, timeman
+from .config import Config
+from .engine import ColumnState, Engine
+from .params import Params
+
+
+class SyntheticForcing:
+    """Seeded diurnal forcing for a ColumnSet (cases.forcing_step), per step."""
+
+    def __init__(self, cols: cases.ColumnSet, seed: int = 0):
+        self.cols, self.seed = cols, seed
+
+    def __call__(self, step: int, t: datetime.datetime) -> np.ndarray:
+        return cases.forcing_step(self.cols, timeman.julian(t), timeman.yearlen(t.year), step,
+                                  seed=self.seed)
+
+
+def _stamp(t: datetime.datetime) -> str:
+    return t.strftime("%Y%m%d%H")
+
+
+def _is_boundary(t: datetime.datetime, t0: datetime.datetime, every) -> bool:
+    if every is None:
+        return False
+    if isinstance(every, str):  # 'Nmonth': calendar month boundaries at 00:00 of day 1
+        n = int(every[:-5])
+        months = (t.year - t0.year) * 12 + (t.month - t0.month)
+        return t.day == 1 and t.hour == 0 and t.minute == 0 and t.second == 0 and months % n == 0 \
+            and t != t0
+    return (t - t0) % every == datetime.timedelta(0)
+
+
+class OfflineDriver:
+    def __init__(self, cfg: Config, cols: cases.ColumnSet, device: int = 0,
+                 params: Params | None = None, forcing=None, precision: int = 4,
+                 math: str = "ref", zsoil=cases.CASE_NML_ZSOIL, write: bool = True):
+        self.cfg = cfg
+        self.engine = Engine(params or Params.builtin(), cfg.engine_options(), device, precision,
+                             math)
+        self.dtype = self.engine.dtype
+        self.dev = torch.device("cuda", device)
+        self.cs = ColumnState.from_host(cols, self.dev, self.dtype)
+        self.forcing = forcing or SyntheticForcing(cols)
+        self.zsoil = [float(z) for z in zsoil]
+        self.dt = cfg.timestep.total_seconds()
+        self.t = cfg.begdatetime
+        self.step_index = 0
+        self.write = write
+        self.diag = torch.zeros((L.NDIAG_OUT, self.cs.ncol), dtype=self.dtype, device=self.dev)
+        self.written = []
+
+    # ---- restart -----------------------------------------------------------------
+    def save_restart(self, path: str):
+        np.savez(path, time=np.array(self.t.isoformat()), step=np.int64(self.step_index),
+                 state=self.cs.state.cpu().numpy(), isnow=self.cs.isnow.cpu().numpy(),
+                 static_f=self.cs.static_f.cpu().numpy(), static_i=self.cs.static_i.cpu().numpy(),
+                 status=self.cs.status.cpu().numpy(), zsoil=np.asarray(self.zsoil, np.float32),
+                 layout=np.array(",".join(n for n, _ in L.STATE_FIELDS)))
+
+    def load_restart(self, path: str):
+        with np.load(path, allow_pickle=False) as z:
+            assert str(z["layout"]) == ",".join(n for n, _ in L.STATE_FIELDS), "state layout"
+            for name in ("state", "isnow", "static_f", "static_i", "status"):
+                getattr(self.cs, name).copy_(torch.as_tensor(z[name], device=self.dev))
+            self.t = datetime.datetime.fromisoformat(str(z["time"]))
+            self.step_index = int(z["step"])
+            self.zsoil = [float(v) for v in z["zsoil"]]
+
+    # ---- time loop -----------------------------------------------------------------
+    def run(self, nsteps: int | None = None):
+        cfg = self.cfg
+        total = cfg.step_count() if nsteps is None else nsteps
+        rank = dist.get_rank() if dist.is_initialized() else 0
+        out_every, res_every = cfg.output_interval, cfg.restart_interval
+        for _ in range(total):
+            if self.t >= cfg.enddatetime:
+                break
+            t0 = self.t
+            t1 = t0 + cfg.timestep
+            out = _is_boundary(t1, cfg.begdatetime, out_every)
+            f = torch.as_tensor(self.forcing(self.step_index, t0), device=self.dev).to(self.dtype)
+            self.engine.step(self.cs, f, self.zsoil, self.dt, timeman.julian(t0),
+                             timeman.yearlen(t0.year), self.diag if out else None,
+                             L.DIAG_OUT_LEVEL if out else L.DIAG_NONE)
+            self.t, self.step_index = t1, self.step_index + 1
+            if out and self.write:
+                d = shard.gather_diag(self.diag) if dist.is_initialized() else self.diag
+                if rank == 0:
+                    os.makedirs(cfg.outdir, exist_ok=True)
+                    path = os.path.join(cfg.outdir, f"{_stamp(t1)}.LDASOUT.npz")
+                    np.savez(path, time=np.array(t1.isoformat()),
+                             fields=np.array(",".join(L.DIAG_OUT)), diag=d.cpu().numpy())
+                    self.written.append(path)
+            if _is_boundary(t1, cfg.begdatetime, res_every) and self.write:
+                os.makedirs(cfg.resdir, exist_ok=True)
+                self.save_restart(os.path.join(cfg.resdir, f"RESTART.{_stamp(t1)}.r{rank}.npz"))
+        torch.cuda.synchronize(self.dev)
+        return self

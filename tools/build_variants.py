@@ -17,6 +17,9 @@ VARIANTS = {
     "w1": ("-DNMP_WAVES_PER_EU=1",),
     "w3": ("-DNMP_WAVES_PER_EU=3",),
     "phase": ("-DNMP_PHASE_TIMING",),
+    "b128": ("-DNMP_BLOCK=128",),
+    "b64": ("-DNMP_BLOCK=64",),
+    "b512": ("-DNMP_BLOCK=512",),
 }
 if __name__ == "__main__":
     names = sys.argv[1:] or list(VARIANTS)
