@@ -69,6 +69,8 @@ def parse():
 def main():
     a = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    # launched by torchrun (even with one rank): take the distributed path
+    use_dist = "RANK" in os.environ and "MASTER_ADDR" in os.environ
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     assert world == a.gpus or world == 1, "launch N>1 with torchrun --nproc-per-node N"
@@ -97,7 +99,7 @@ def main():
 
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    if world > 1:
+    if use_dist:
         dist.init_process_group("nccl", device_id=dev)
     dtype = torch.float32 if a.precision == 4 else torch.float64
     eng = Engine(P, L.CASE_NML_OPTIONS, device=local, precision=a.precision, math=a.math)
@@ -109,10 +111,10 @@ def main():
             cols, julian0 + s * a.dt / 86400.0, yearlen, s, seed=seed)))
     diag = [torch.zeros((L.NDIAG_OUT, n), dtype=dtype, device=dev) for _ in range(2)]
     gathered = [torch.empty((world * L.NDIAG_OUT, n), dtype=dtype, device=dev) for _ in range(2)] \
-        if world > 1 else None
+        if use_dist else None
     pending = [None, None]
     compute = torch.cuda.Stream(dev)
-    comm = torch.cuda.Stream(dev) if world > 1 else None
+    comm = torch.cuda.Stream(dev) if use_dist else None
     del cols
 
     def step(k, ev=None):
@@ -130,7 +132,7 @@ def main():
                      L.DIAG_OUT_LEVEL if out else L.DIAG_NONE, stream=compute)
             if ev is not None:
                 ev[1].record(compute)
-        if out and world > 1:
+        if out and use_dist:
             comm.wait_stream(compute)
             with torch.cuda.stream(comm):
                 _, pending[b] = shard.gather_diag(diag[b], gathered[b], async_op=True)
@@ -139,7 +141,7 @@ def main():
     for k in range(a.warmup):
         step(k)
     torch.cuda.synchronize(dev)
-    if world > 1:
+    if use_dist:
         dist.barrier()
     torch.cuda.synchronize(dev)
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
@@ -152,14 +154,14 @@ def main():
         if p is not None:
             p.wait()
     torch.cuda.synchronize(dev)
-    if world > 1:
+    if use_dist:
         dist.barrier()
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
     kern_ms = float(np.mean([e0.elapsed_time(e1) for e0, e1 in evs]))
     st_bad = int((cs.status != 0).sum().item())
     finite = bool(torch.isfinite(cs.state[L.s("STC")]).all().item())
-    if world > 1:
+    if use_dist:
         t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, kern_ms = float(t[0]), float(t[1])
@@ -202,7 +204,7 @@ def main():
         }
         print(json.dumps(line), flush=True)
     eng.close()
-    if world > 1:
+    if use_dist:
         dist.destroy_process_group()
 
 
