@@ -59,6 +59,10 @@ def parse():
     ap.add_argument("--dt", type=float, default=1800.0)
     ap.add_argument("--out-every", type=int, default=2, help="output (diag) step interval")
     ap.add_argument("--period", type=int, default=48, help="resident forcing slices (cycled)")
+    ap.add_argument("--order", default="as-generated", choices=("as-generated", "lon", "lon-type"),
+                    help="column order on the GPU (columns are independent: any permutation "
+                         "gives bit-identical per-column results); 'lon' groups columns of "
+                         "similar solar time into the same wave, like a real lat-lon grid")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-steps", type=int, default=32)
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic.json"),
@@ -81,6 +85,13 @@ def main():
     options = L.options_tuple(L.CASE_NML_OPTIONS)
     julian0, yearlen, seed = 180.0, 366, 1000 + rank
     cols = cases.make_columns(a.ncol, a.kind, pdict, seed=seed, julian=julian0)
+    if a.order != "as-generated":
+        key = np.round(np.degrees(cols.lon) / 2.0)  # 2-degree longitude bands
+        if a.order == "lon-type":
+            perm = np.lexsort((cols.static_i[L.STATIC_I.index("VEGTYP")], key))
+        else:
+            perm = np.argsort(cols.lon, kind="stable")
+        cols = cols.take(perm)
 
     # ---- CPU baseline (rank 0, N=1), BEFORE anything touches the GPU ------
     cpu = None
@@ -194,7 +205,8 @@ def main():
                        f"{n} {a.kind} columns/GPU, 4 soil + 3 snow layers", "kind": a.kind,
                        "ncol_per_gpu": n,
                        "ncol_total": world * n, "dt_s": a.dt, "out_every": a.out_every,
-                       "math": a.math, "parallelism": f"column-shard x{world}"},
+                       "math": a.math, "column_order": a.order,
+                       "parallelism": f"column-shard x{world}"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": "sflx_step_kernel", "kernel_ms": kern_ms,
