@@ -16,6 +16,8 @@
  *                             noahmp_set_options            core/module_noahmp_global.f90:77-112
  * nmp_step                    noahmp_run                    core/module_noahmp_engine.f90:8-10
  *                             = noahmp_sflx over every column core/module_noahmp_func.f90:66-476
+ * nmp_run, nmp_run_out        the offline time loop around noahmp_run (run/main.py:12-14
+ *                             stops after the namelist): many steps, one launch
  * nmp_state_from_aos          layout bridge from noahmp_state_t records
  *                                                           core/module_noahmp_type.f90:10-42
  * nmp_finalize, nmp_strerror  (error path of utils `assert`/`stop`, core/module_noahmp_utils.f90:21-53)
@@ -48,7 +50,7 @@
 extern "C" {
 #endif
 
-#define NMP_ABI_VERSION 1
+#define NMP_ABI_VERSION 2
 
 /* ---- dimensions (core/module_noahmp_global.f90:9-13) -------------------- */
 #define NMP_NSOIL 4
@@ -202,14 +204,28 @@ int nmp_step(nmp_engine* eng, int64_t ncol, int64_t ld, const float zsoil[4], fl
              const int32_t* static_i, const void* forcing, void* diag, int diag_level,
              int32_t* col_status, void* stream);
 
-/* Same step, many times: nsteps steps whose forcing slices are
- * forcing + s*forcing_stride (elements, real type), julian advancing by
- * dt/86400 per step.  diag (if non-NULL) receives the last step only. */
+/* Same step, many times: nsteps steps (one launch each, enqueued on stream)
+ * whose forcing slices are forcing + (s % forcing_period)*forcing_stride
+ * (elements, real type; forcing_period 0 = nsteps distinct slices), julian
+ * advancing by dt/86400 per step (julian0 + (float)s*dt/86400.0f); bitwise the
+ * same as nsteps nmp_step calls.  diag (if non-NULL) receives the last step only. */
 int nmp_run(nmp_engine* eng, int64_t ncol, int64_t ld, const float zsoil[4], float dt,
             float julian0, int32_t yearlen, int32_t nsteps, void* state, int32_t* isnow,
             const void* static_f, const int32_t* static_i, const void* forcing,
             int64_t forcing_stride, int32_t forcing_period, void* diag, int diag_level,
             int32_t* col_status, void* stream);
+
+/* nmp_run with periodic output: every step s with (s+1) % out_every == 0
+ * writes its diagnostics (diag_level) to slot ((s+1)/out_every - 1) % diag_slots
+ * of the ring diag + slot*diag_stride (elements; >= the diag block size
+ * x ld when more than one slot is written).  nmp_run is out_every = nsteps,
+ * diag_slots = 1. */
+int nmp_run_out(nmp_engine* eng, int64_t ncol, int64_t ld, const float zsoil[4], float dt,
+                float julian0, int32_t yearlen, int32_t nsteps, void* state, int32_t* isnow,
+                const void* static_f, const int32_t* static_i, const void* forcing,
+                int64_t forcing_stride, int32_t forcing_period, void* diag, int diag_level,
+                int32_t out_every, int32_t diag_slots, int64_t diag_stride, int32_t* col_status,
+                void* stream);
 
 /* Host-side converter: n byte-identical `noahmp_state_t` sequence records
  * (168 B each, core/module_noahmp_type.f90:10-42) -> host SoA float state

@@ -20,7 +20,11 @@ HEADERS = ["dev_params.h", "sflx_kargs.h", "sflx_math.h", "glibc_math.h"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")
 FLAGS = ["-O3", f"--offload-arch={ARCH}", "-fPIC", "-shared", "-std=c++17",
-         "-ffp-contract=off", "-Wno-unused-result", "-Wno-unused-value"]
+         "-ffp-contract=off", "-Wno-unused-result", "-Wno-unused-value",
+         # MachineLICM hoists uniform offsets/constants out of the step and
+         # Newton loops and holds them across the whole step: spills 70 -> 42
+         # (single-step kernel) without it
+         "-mllvm", "-disable-machine-licm"]
 
 
 def source_hash() -> str:

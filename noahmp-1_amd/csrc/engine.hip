@@ -93,6 +93,19 @@ int launch(const nmp_engine* e, int64_t ncol, int64_t ld, const float zsoil[4], 
   return err == hipSuccess ? NMP_OK : NMP_E_DEVICE;
 }
 
+int check_common(const nmp_engine* eng, int64_t ncol, int64_t ld, const float zsoil[4], float dt,
+                 int32_t yearlen, const void* state, const int32_t* isnow, const void* static_f,
+                 const int32_t* static_i, const void* forcing, const void* diag, int diag_level,
+                 const int32_t* col_status) {
+  if (!zsoil || ld < ncol || !state || !isnow || !static_f || !static_i || !forcing || !col_status)
+    return NMP_E_ARG;
+  if (diag_level < NMP_DIAG_NONE || diag_level > NMP_DIAG_FULL) return NMP_E_ARG;
+  if (diag_level != NMP_DIAG_NONE && !diag) return NMP_E_ARG;
+  if (!(dt > 0.0f) || yearlen <= 0) return NMP_E_ARG;
+  if (ensure_device(eng->device) != NMP_OK) return NMP_E_DEVICE;
+  return NMP_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -164,12 +177,9 @@ int nmp_step(nmp_engine* eng, int64_t ncol, int64_t ld, const float zsoil[4], fl
              int32_t* col_status, void* stream) {
   if (!eng || ncol < 0) return NMP_E_ARG;
   if (ncol == 0) return NMP_OK;
-  if (!zsoil || ld < ncol || !state || !isnow || !static_f || !static_i || !forcing || !col_status)
-    return NMP_E_ARG;
-  if (diag_level < NMP_DIAG_NONE || diag_level > NMP_DIAG_FULL) return NMP_E_ARG;
-  if (diag_level != NMP_DIAG_NONE && !diag) return NMP_E_ARG;
-  if (!(dt > 0.0f) || yearlen <= 0) return NMP_E_ARG;
-  if (ensure_device(eng->device) != NMP_OK) return NMP_E_DEVICE;
+  int rc = check_common(eng, ncol, ld, zsoil, dt, yearlen, state, isnow, static_f, static_i,
+                        forcing, diag, diag_level, col_status);
+  if (rc != NMP_OK) return rc;
   return launch(eng, ncol, ld, zsoil, dt, julian, yearlen, state, isnow, static_f, static_i,
                 forcing, diag, diag_level, col_status, static_cast<hipStream_t>(stream));
 }
@@ -179,15 +189,50 @@ int nmp_run(nmp_engine* eng, int64_t ncol, int64_t ld, const float zsoil[4], flo
             const void* static_f, const int32_t* static_i, const void* forcing,
             int64_t forcing_stride, int32_t forcing_period, void* diag, int diag_level,
             int32_t* col_status, void* stream) {
-  if (!eng || nsteps < 0 || forcing_stride < 0 || forcing_period < 0) return NMP_E_ARG;
+  // diagnostics of the last step only = one output every nsteps steps, one slot
+  return nmp_run_out(eng, ncol, ld, zsoil, dt, julian0, yearlen, nsteps, state, isnow, static_f,
+                     static_i, forcing, forcing_stride, forcing_period, diag, diag_level,
+                     nsteps > 0 ? nsteps : 1, 1, 0, col_status, stream);
+}
+
+int nmp_run_out(nmp_engine* eng, int64_t ncol, int64_t ld, const float zsoil[4], float dt,
+                float julian0, int32_t yearlen, int32_t nsteps, void* state, int32_t* isnow,
+                const void* static_f, const int32_t* static_i, const void* forcing,
+                int64_t forcing_stride, int32_t forcing_period, void* diag, int diag_level,
+                int32_t out_every, int32_t diag_slots, int64_t diag_stride, int32_t* col_status,
+                void* stream) {
+  if (!eng || ncol < 0 || nsteps < 0 || forcing_stride < 0 || forcing_period < 0)
+    return NMP_E_ARG;
+  if (out_every < 1 || diag_slots < 1 || diag_stride < 0) return NMP_E_ARG;
+  if (ncol == 0 || nsteps == 0) return NMP_OK;
+  // forcing slices and diag slots must not overlap the columns they follow
+  const int32_t nslices = forcing_period > 0 ? forcing_period : nsteps;
+  if (nslices > 1 && forcing_stride < NMP_NFORCING * ld) return NMP_E_ARG;
+  const int32_t nout = nsteps / out_every;
+  if (diag_level != NMP_DIAG_NONE && nout > 1 && diag_slots > 1) {
+    const int64_t nd = diag_level == NMP_DIAG_FULL ? NMP_NDIAG_FULL : NMP_NDIAG_OUT;
+    if (diag_stride < nd * ld) return NMP_E_ARG;
+  }
+  int rc = check_common(eng, ncol, ld, zsoil, dt, yearlen, state, isnow, static_f, static_i,
+                        forcing, diag, diag_level, col_status);
+  if (rc != NMP_OK) return rc;
+  // One launch per step, enqueued back to back on `stream`.  (A single
+  // multi-step launch that keeps each block on its columns for all steps was
+  // measured slower on the mixed-column benchmark: per-block cost differences
+  // persist across steps, whereas per-step launches rebalance blocks over CUs
+  // every step -- DESIGN.md "Launch structure".)
   const size_t esz = eng->precision == 4 ? 4 : 8;
+  const auto hs = static_cast<hipStream_t>(stream);
   for (int32_t s = 0; s < nsteps; ++s) {
     const int32_t fs = forcing_period > 0 ? s % forcing_period : s;
     const char* f = static_cast<const char*>(forcing) + (size_t)fs * forcing_stride * esz;
     const float jul = julian0 + (float)s * dt / 86400.0f;
-    const int lvl = (s == nsteps - 1) ? diag_level : NMP_DIAG_NONE;
-    int rc = nmp_step(eng, ncol, ld, zsoil, dt, jul, yearlen, state, isnow, static_f, static_i, f,
-                      diag, lvl, col_status, stream);
+    const bool out = diag_level != NMP_DIAG_NONE && (s + 1) % out_every == 0;
+    char* d = out ? static_cast<char*>(diag) +
+                        (size_t)(((s + 1) / out_every - 1) % diag_slots) * diag_stride * esz
+                  : nullptr;
+    rc = launch(eng, ncol, ld, zsoil, dt, jul, yearlen, state, isnow, static_f, static_i, f, d,
+                out ? diag_level : NMP_DIAG_NONE, col_status, hs);
     if (rc != NMP_OK) return rc;
   }
   return NMP_OK;

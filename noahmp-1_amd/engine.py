@@ -127,16 +127,36 @@ class Engine:
 
     def run(self, cs: ColumnState, forcings: torch.Tensor, zsoil, dt: float, julian0: float,
             yearlen: int, nsteps: int, diag: torch.Tensor | None = None,
-            diag_level: int = L.DIAG_NONE, stream=None):
-        """nsteps steps cycling through forcings[(period, 12, n)] (last-step diagnostics)."""
+            diag_level: int = L.DIAG_NONE, stream=None, out_every: int | None = None):
+        """nsteps steps in one launch, cycling through forcings[(period, 12, n)].
+
+        Diagnostics: with `out_every` None, `diag` (nd, n) receives the last step
+        (nmp_run); otherwise every out_every-th step writes the next slot of the
+        ring `diag` (slots, nd, n), wrapping (nmp_run_out)."""
         n = cs.ncol
         assert forcings.dim() == 3
         self._check_cols(cs, forcings[0])
         zs = (C.c_float * 4)(*[float(z) for z in zsoil])
         s = stream if stream is not None else torch.cuda.current_stream(self.device)
-        _lib.check(self._lib.nmp_run(self._h, n, n, zs, float(dt), float(julian0), int(yearlen),
-                                     int(nsteps), _ptr(cs.state), _ptr(cs.isnow),
-                                     _ptr(cs.static_f), _ptr(cs.static_i), _ptr(forcings),
-                                     L.NFORCING * n, forcings.shape[0], _ptr(diag),
-                                     int(diag_level), _ptr(cs.status),
-                                     C.c_void_p(s.cuda_stream)), "nmp_run")
+        if diag_level != L.DIAG_NONE:
+            nd = L.NDIAG_FULL if diag_level == L.DIAG_FULL_LEVEL else L.NDIAG_OUT
+            assert diag is not None and diag.dtype == self.dtype and diag.is_contiguous()
+            assert diag.shape[-2:] == (nd, n) and diag.dim() == (2 if out_every is None else 3)
+            assert diag.device.type == "cuda" and diag.device.index == self.device
+        if out_every is None:
+            _lib.check(self._lib.nmp_run(self._h, n, n, zs, float(dt), float(julian0), int(yearlen),
+                                         int(nsteps), _ptr(cs.state), _ptr(cs.isnow),
+                                         _ptr(cs.static_f), _ptr(cs.static_i), _ptr(forcings),
+                                         L.NFORCING * n, forcings.shape[0], _ptr(diag),
+                                         int(diag_level), _ptr(cs.status),
+                                         C.c_void_p(s.cuda_stream)), "nmp_run")
+            return
+        slots = diag.shape[0] if diag is not None else 1
+        dstride = diag[0].numel() if diag is not None else 0
+        _lib.check(self._lib.nmp_run_out(self._h, n, n, zs, float(dt), float(julian0),
+                                         int(yearlen), int(nsteps), _ptr(cs.state),
+                                         _ptr(cs.isnow), _ptr(cs.static_f), _ptr(cs.static_i),
+                                         _ptr(forcings), L.NFORCING * n, forcings.shape[0],
+                                         _ptr(diag), int(diag_level), int(out_every), int(slots),
+                                         int(dstride), _ptr(cs.status),
+                                         C.c_void_p(s.cuda_stream)), "nmp_run_out")

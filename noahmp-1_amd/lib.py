@@ -84,6 +84,11 @@ def load(build_if_missing: bool = False):
     lib.nmp_run.argtypes = [vp, C.c_int64, C.c_int64, f32p, C.c_float, C.c_float, C.c_int32,
                             C.c_int32, vp, vp, vp, vp, vp, C.c_int64, C.c_int32, vp, C.c_int, vp,
                             vp]
+    if hasattr(lib, "nmp_run_out"):  # (absent from ABI-1 builds timed by tools/sweep.sh)
+        lib.nmp_run_out.argtypes = [vp, C.c_int64, C.c_int64, f32p, C.c_float, C.c_float,
+                                    C.c_int32, C.c_int32, vp, vp, vp, vp, vp, C.c_int64,
+                                    C.c_int32, vp, C.c_int, C.c_int32, C.c_int32, C.c_int64, vp,
+                                    vp]
     lib.nmp_state_from_aos.argtypes = [vp, C.c_int64, C.c_int64, vp, vp, vp]
     lib.nmp_engine_info.argtypes = [vp, C.POINTER(C.c_int), C.POINTER(C.c_int),
                                     C.POINTER(NmpOptions)]
@@ -96,7 +101,8 @@ def load(build_if_missing: bool = False):
     return lib
 
 
-EXPORTED_SYMBOLS = ["nmp_read_tables", "nmp_init", "nmp_step", "nmp_run", "nmp_state_from_aos",
+EXPORTED_SYMBOLS = ["nmp_read_tables", "nmp_init", "nmp_step", "nmp_run", "nmp_run_out",
+                    "nmp_state_from_aos",
                     "nmp_engine_info", "nmp_set_math", "nmp_finalize", "nmp_strerror",
                     "nmp_abi_version"]
 

@@ -195,6 +195,40 @@ def test_run_equals_repeated_step(engines):
     assert torch.equal(da, db) and torch.equal(a.status, b.status)
 
 
+def test_run_out_ring_equals_repeated_step(engines):
+    """nmp_run_out == 12 nmp_step calls, bitwise: state, ISNOW, status, and each
+    output step's diagnostics in its ring slot (out_every 3, 3 slots: the 4th
+    output wraps onto slot 0); 200,003 columns = a ragged last block."""
+    from noahmp_amd.engine import ColumnState
+    from noahmp_amd.params import Params
+    n, nsteps, every, slots = 200_003, 12, 3, 3
+    opts = L.CASE_NML_OPTIONS
+    eng = engines([opts[k] for k in L.OPTION_NAMES])
+    cols = cases.make_columns(n, "mixed", Params.builtin().as_dict(), seed=5, julian=100.0)
+    F = torch.stack([torch.as_tensor(cases.forcing_step(cols, 100.0 + s * 1800.0 / 86400.0, 365,
+                                                        s, seed=5)) for s in range(5)]).to(DEV)
+    a = ColumnState.from_host(cols, DEV)
+    b = ColumnState.from_host(cols, DEV)
+    ring = torch.full((slots, L.NDIAG_OUT, n), float("nan"), device=DEV)
+    eng.run(a, F, cases.CASE_NML_ZSOIL, 1800.0, 100.0, 365, nsteps, ring, L.DIAG_OUT_LEVEL,
+            out_every=every)
+    expect = {}
+    d = torch.zeros((L.NDIAG_OUT, n), device=DEV)
+    for s in range(nsteps):
+        out = (s + 1) % every == 0
+        jul = float(np.float32(100.0) + np.float32(s) * np.float32(1800.0) / np.float32(86400.0))
+        eng.step(b, F[s % 5], cases.CASE_NML_ZSOIL, 1800.0, jul, 365, d if out else None,
+                 L.DIAG_OUT_LEVEL if out else L.DIAG_NONE)
+        if out:
+            expect[((s + 1) // every - 1) % slots] = d.clone()
+    torch.cuda.synchronize()
+    bits = lambda t: t.view(torch.int32)  # NaN-safe bitwise comparison
+    assert torch.equal(bits(a.state), bits(b.state)) and torch.equal(a.isnow, b.isnow)
+    assert torch.equal(a.status, b.status)
+    for k in range(slots):
+        assert torch.equal(bits(ring[k]), bits(expect[k])), k
+
+
 def test_diag_levels_consistent(engines):
     """DIAG_OUT fields are the DIAG_FULL values (T2M = the fveg blend of T2MV/T2MB)."""
     from noahmp_amd.engine import ColumnState

@@ -20,6 +20,8 @@ VARIANTS = {
     "b128": ("-DNMP_BLOCK=128",),
     "b64": ("-DNMP_BLOCK=64",),
     "b512": ("-DNMP_BLOCK=512",),
+    "mlicm": ("-mllvm", "-disable-machine-licm=false"),
+    "w4_mlicm": ("-DNMP_WAVES_PER_EU=4", "-mllvm", "-disable-machine-licm=false"),
 }
 if __name__ == "__main__":
     names = sys.argv[1:] or list(VARIANTS)
