@@ -24,6 +24,21 @@ typedef ORACLE_REAL real;
 #define ORACLE_IS_FLOAT (sizeof(real) == 4)
 #define K(x) ((real)(ORACLE_IS_FLOAT ? (double)(x##f) : (x)))
 
+/* Loop trip counts per column (tools/iter_stats.py; build with -DORACLE_ITER_STATS
+ * only): 0 vege_flux Newton, 1 stomata bisection, 2 frh2o, 3 soilwater
+ * sub-steps, 4 bare_flux Newton. */
+#ifdef ORACLE_ITER_STATS
+static int32_t* g_stats;
+static int32_t g_stat_col;
+void oracle_set_stats(int32_t* buf) { g_stats = buf; }
+#define ITER_STAT(k)                                        \
+  do {                                                      \
+    if (g_stats) g_stats[(size_t)g_stat_col * 8 + (k)]++;   \
+  } while (0)
+#else
+#define ITER_STAT(k) ((void)0)
+#endif
+
 #if defined(ORACLE_DOUBLE)
 #define EXP exp
 #define LOG log
@@ -787,7 +802,7 @@ static void stomata(const nmp_params* P, int lutyp, real igs, real sfcprs, real 
   real rlb = rb / cf;
   real cihigh = K(1.5) * co2, cilow = K(0.0);
   const int c3c4 = P->c3c4[lutyp - 1];
-  for (int iter = 1; iter <= 20; ++iter) {
+  for (int iter = 1; iter <= 20; ++iter) { ITER_STAT(1);
     real ci = K(0.5) * (cihigh + cilow);
     /* ci2ci: func.f90:3847-3886.  The reference keeps wc/wj/we SAVEd (nan4
      * initialised); for C3C4 outside {1,2} we use that initial NaN. */
@@ -902,7 +917,7 @@ static void vege_flux(ctx_t* X, int ISNOW, int lutyp, real DT, real SAV, real SA
   real AIR = -EMV * (K(1.0) + (K(1.0) - EMV) * (K(1.0) - EMG)) * LWDN - EMV * EMG * SB * p4(*TG);
   real CIR = (K(2.0) - EMV * (K(1.0) - EMG)) * EMV * SB;
 
-  for (int iter = 1; iter <= NITERC; ++iter) {
+  for (int iter = 1; iter <= NITERC; ++iter) { ITER_STAT(0);
     Z0H = Z0M;
     Z0HG = Z0MG;
     if (X->O->opt_sfc == 1)
@@ -986,7 +1001,7 @@ static void vege_flux(ctx_t* X, int ISNOW, int lutyp, real DT, real SAV, real SA
   CEV = RHOAIR * CPAIR / (GAMMAG * (RAWG + RSURF));
   CGH = K(2.0) * DF[ISNOW + 1] / DZSNSO[ISNOW + 1];
   ESTG = K(0.0);
-  for (int iter = 1; iter <= NITERG; ++iter) {
+  for (int iter = 1; iter <= NITERG; ++iter) { ITER_STAT(4);
     T = tdc(*TG);
     esat(T, &ESATW, &ESATI, &DSATW, &DSATI);
     if (T > K(0.0)) {
@@ -1229,7 +1244,7 @@ static real frh2o(ctx_t* X, int sltyp, real TKELV, real SMC, real soilwat) {
     real SWL = SMC - soilwat;
     if (SWL > (SMC - K(0.02))) SWL = SMC - K(0.02);
     if (SWL < K(0.0)) SWL = K(0.0);
-    while ((NLOG < 10) && (KCOUNT == 0)) {
+    while ((NLOG < 10) && (KCOUNT == 0)) { ITER_STAT(2);
       NLOG = NLOG + 1;
       real DF = LOG((SOILP(psisat) * GRAV / HFUS) * p2(K(1.0) + CK * SWL) *
                     POW(SOILP(smcmax) / (SMC - SWL), BX)) -
@@ -2113,7 +2128,7 @@ static void soilh2o(ctx_t* X, int sltyp, int lutyp, real dt, const real* zsoil,
   }
   real dtfine = dt / (real)niter;
   real QDRAIN_SAVE = K(0.0);
-  for (int iter = 1; iter <= niter; ++iter) {
+  for (int iter = 1; iter <= niter; ++iter) { ITER_STAT(3);
     real WPLUS;
     srt(X, sltyp, zsoil, slptyp, qinfil, ETRANI, QSEVA, soilwat, SMC, FCR, SICEMAX, *FCRMAX,
         RHSTT, AI, BI, CI, QDRAIN, WCND);
@@ -2734,6 +2749,9 @@ int oracle_sflx_batch(int32_t n, real dt, int32_t yearlen, real julian, const re
                       real* st, int32_t* isnow, const real* sf, const int32_t* si, const real* fc,
                       real* dg, int32_t* status, const nmp_params* P, const nmp_options* O) {
   for (int32_t c = 0; c < n; ++c) {
+#ifdef ORACLE_ITER_STATS
+    g_stat_col = c;
+#endif
     ctx_t X = {P, O, 0};
     sflx_column(&X, dt, yearlen, julian, zsoil, st + (size_t)c * NMP_NSTATE, isnow + c,
                 sf + (size_t)c * NMP_NSTATIC_F, si + (size_t)c * NMP_NSTATIC_I,

@@ -12,9 +12,15 @@ noahmp_amd.cases.  Each .npz holds inputs AND the reference outputs.
   traj_casenml.npz              96 steps (run/case.nml length, dt=900 s) of the
                                 case.nml column + 31 mixed columns, every step
   traj_snow.npz                 480 steps (dt=1800 s) of 24 snow columns
+  single_combo_*.npz            several non-default options at once (hand-picked and seeded)
+  single_tbl_<name>.npz         the other parameter tables (MODIS/IGBP veg, STAS-RUC soil);
+                                the fixture records its `soil`/`veg` table tags
+  traj_combo_a.npz              48 steps (dt=1800 s) of 32 columns under combo_a
+                                (dynamic vegetation + carbon, Chen97 surface layer, ...)
 
 usage (this container only; needs /root/reference):
-  make -C oracle ref && python tests/golden/make_golden.py
+  make -C oracle ref && python tests/golden/make_golden.py [group ...]
+  groups: params single variants traj combos tables (default: all)
 """
 from __future__ import annotations
 
@@ -45,6 +51,18 @@ VARIANTS = {
     "alb1": dict(opt_alb=1), "snf2": dict(opt_snf=2), "snf3": dict(opt_snf=3),
     "tbot2": dict(opt_tbot=2), "stc2": dict(opt_stc=2),
 }
+# several non-default options in one configuration (interactions between options)
+COMBOS = {
+    "combo_a": dict(opt_veg=2, opt_crs=2, opt_btr=2, opt_run=3, opt_sfc=2, opt_frz=2, opt_inf=2,
+                    opt_rad=1, opt_alb=1, opt_snf=2, opt_tbot=2, opt_stc=2),
+    "combo_b": dict(opt_veg=5, opt_btr=3, opt_run=2, opt_rad=3, opt_snf=3),
+    "combo_c": dict(opt_veg=4, opt_run=4, opt_rad=2, opt_sfc=2, opt_stc=2, opt_frz=2),
+}
+OPTION_VALUES = dict(opt_veg=5, opt_crs=2, opt_btr=3, opt_run=4, opt_sfc=2, opt_frz=2, opt_inf=2,
+                     opt_rad=3, opt_alb=2, opt_snf=3, opt_tbot=2, opt_stc=2)
+# (name, soil tag, veg tag) for single calls with the other shipped tables
+TABLE_CASES = [("modis", "STAS", "MODIFIED_IGBP_MODIS_NOAH"), ("ruc", "STAS-RUC", "USGS"),
+               ("modis_ruc", "STAS-RUC", "MODIFIED_IGBP_MODIS_NOAH")]
 TAGS = [("STAS", "USGS"), ("STAS-RUC", "USGS"), ("STAS", "MODIFIED_IGBP_MODIS_NOAH"),
         ("STAS-RUC", "MODIFIED_IGBP_MODIS_NOAH")]
 
@@ -61,15 +79,22 @@ def save(name, **arrays):
     print("wrote", path, os.path.getsize(path) // 1024, "KB")
 
 
-def single(name, P, kind, n, seed, options, dt=1800.0, julian=180.3, yearlen=366, soldn=None):
+def random_combo(seed):
+    rng = np.random.default_rng(seed)
+    return {k: int(rng.integers(1, v + 1)) for k, v in OPTION_VALUES.items()}
+
+
+def single(name, P, kind, n, seed, options, dt=1800.0, julian=180.3, yearlen=366, soldn=None,
+           tags=("STAS", "USGS")):
     cols = cases.make_columns(n, kind, P, seed=seed, julian=julian)
     f = cases.forcing_random(cols, seed=seed)
     if soldn is not None:  # extreme shortwave -> ERRSW / ERRENG / FIRE fatal-status columns
         f[L.FORCING.index("SOLDN")] = np.random.default_rng(seed).uniform(*soldn, n)
-    ref.configure(options)
+    ref.configure(options, *tags)
     st, isn, dg, status = ref.step(cases.CASE_NML_ZSOIL, dt, yearlen, julian, cols.state,
                                    cols.isnow, cols.static_f, cols.static_i, f)
     save(f"single_{name}.npz", options=np.array(options, np.int32), dt=np.float32(dt),
+         soil=np.array(tags[0]), veg=np.array(tags[1]),
          julian=np.float32(julian), yearlen=np.int32(yearlen), zsoil=cases.CASE_NML_ZSOIL,
          state0=cols.state, isnow0=cols.isnow, static_f=cols.static_f, static_i=cols.static_i,
          forcing=f, state1=st, isnow1=isn, diag=dg, status=status)
@@ -97,6 +122,11 @@ def trajectory(name, P, cols, nsteps, dt, julian0, yearlen, seed, options, keep_
          states=np.stack(S), isnows=np.stack(I), diags=np.stack(D), statuses=np.stack(ST))
 
 
+def table_child(name, soil, veg, seed):
+    ref.configure(BASE, soil, veg)
+    single(f"tbl_{name}", ref.dump_params(), "conus", 512, seed, BASE, tags=(soil, veg))
+
+
 def dump_params_child(soil, veg):
     ref.configure(BASE, soil, veg)
     d = ref.dump_params()
@@ -107,25 +137,44 @@ if __name__ == "__main__":
     if len(sys.argv) == 4 and sys.argv[1] == "--params":
         dump_params_child(sys.argv[2], sys.argv[3])
         sys.exit(0)
+    if len(sys.argv) == 6 and sys.argv[1] == "--table":
+        table_child(sys.argv[2], sys.argv[3], sys.argv[4], int(sys.argv[5]))
+        sys.exit(0)
+    groups = set(sys.argv[1:]) or {"params", "single", "variants", "traj", "combos", "tables"}
     # the reference keeps tables in process-global module arrays: one process per tag pair
-    for soil, veg in TAGS:
-        subprocess.run([sys.executable, __file__, "--params", soil, veg], check=True)
+    if "params" in groups:
+        for soil, veg in TAGS:
+            subprocess.run([sys.executable, __file__, "--params", soil, veg], check=True)
     ref.configure(BASE)
     P = ref.dump_params()
-    single("casenml_mixed", P, "mixed", 2048, 11, BASE)
-    single("casenml_conus", P, "conus", 2048, 12, BASE)
-    single("fatal", P, "conus", 256, 13, BASE, soldn=(0.0, 2.0e5))
-    for i, (name, kw) in enumerate(VARIANTS.items()):
-        single(name, P, "conus", 256, 100 + i, opts_with(**kw))
-    # 96-step case.nml trajectory (interval_seconds = 900, 2000-01-01 .. 01-02)
-    c1 = cases.make_columns(1, "casenml", P, seed=0, julian=0.0)
-    c2 = cases.make_columns(31, "mixed", P, seed=21, julian=0.0)
-    cols = cases.ColumnSet(*[np.concatenate([a, b], axis=-1) for a, b in zip(
-        (c1.static_f, c1.static_i, c1.state, c1.isnow, c1.lon, c1.t0, c1.amp, c1.rh, c1.pres,
-         c1.wind, c1.wet),
-        (c2.static_f, c2.static_i, c2.state, c2.isnow, c2.lon, c2.t0, c2.amp, c2.rh, c2.pres,
-         c2.wind, c2.wet))])
-    trajectory("casenml", P, cols, 96, 900.0, 0.0, 366, 5, BASE)
-    snow = cases.make_columns(400, "conus", P, seed=33, julian=15.0)
-    pick = np.nonzero(snow.isnow < 0)[0][:24]
-    trajectory("snow", P, snow.take(pick), 480, 1800.0, 15.0, 366, 7, BASE, keep_every=8)
+    if "single" in groups:
+        single("casenml_mixed", P, "mixed", 2048, 11, BASE)
+        single("casenml_conus", P, "conus", 2048, 12, BASE)
+        single("fatal", P, "conus", 256, 13, BASE, soldn=(0.0, 2.0e5))
+    if "variants" in groups:
+        for i, (name, kw) in enumerate(VARIANTS.items()):
+            single(name, P, "conus", 256, 100 + i, opts_with(**kw))
+    if "traj" in groups:
+        # 96-step case.nml trajectory (interval_seconds = 900, 2000-01-01 .. 01-02)
+        c1 = cases.make_columns(1, "casenml", P, seed=0, julian=0.0)
+        c2 = cases.make_columns(31, "mixed", P, seed=21, julian=0.0)
+        cols = cases.ColumnSet(*[np.concatenate([a, b], axis=-1) for a, b in zip(
+            (c1.static_f, c1.static_i, c1.state, c1.isnow, c1.lon, c1.t0, c1.amp, c1.rh, c1.pres,
+             c1.wind, c1.wet),
+            (c2.static_f, c2.static_i, c2.state, c2.isnow, c2.lon, c2.t0, c2.amp, c2.rh, c2.pres,
+             c2.wind, c2.wet))])
+        trajectory("casenml", P, cols, 96, 900.0, 0.0, 366, 5, BASE)
+        snow = cases.make_columns(400, "conus", P, seed=33, julian=15.0)
+        pick = np.nonzero(snow.isnow < 0)[0][:24]
+        trajectory("snow", P, snow.take(pick), 480, 1800.0, 15.0, 366, 7, BASE, keep_every=8)
+    if "combos" in groups:
+        for i, (name, kw) in enumerate(COMBOS.items()):
+            single(name, P, "conus", 512, 200 + i, opts_with(**kw))
+        for i in range(3):
+            single(f"combo_r{i}", P, "conus", 512, 300 + i, opts_with(**random_combo(300 + i)))
+        cols = cases.make_columns(32, "conus", P, seed=41, julian=120.0)
+        trajectory("combo_a", P, cols, 48, 1800.0, 120.0, 366, 9, opts_with(**COMBOS["combo_a"]))
+    if "tables" in groups:
+        for i, (name, soil, veg) in enumerate(TABLE_CASES):
+            subprocess.run([sys.executable, __file__, "--table", name, soil, veg, str(400 + i)],
+                           check=True)

@@ -18,6 +18,16 @@ def load_params(veg: str = "USGS", soil: str = "STAS") -> dict:
     return load(f"params_ref_{veg}_{soil}.npz")
 
 
+def fixture_tags(g: dict) -> tuple[str, str]:
+    """(soil, veg) parameter-table tags a fixture was generated with (default STAS/USGS)."""
+    return (str(g["soil"]) if "soil" in g else "STAS", str(g["veg"]) if "veg" in g else "USGS")
+
+
+def fixture_params(g: dict) -> dict:
+    soil, veg = fixture_tags(g)
+    return load_params(veg, soil)
+
+
 def single_names() -> list[str]:
     return sorted(os.path.basename(p)[7:-4] for p in glob.glob(os.path.join(GOLDEN, "single_*.npz")))
 

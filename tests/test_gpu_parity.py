@@ -23,8 +23,8 @@ import numpy as np
 import pytest
 import torch
 
-from golden_io import (as_ref_status, bit_equal, close, column_mismatch, load, load_params,
-                       parity_vs_reference, single_names)
+from golden_io import (as_ref_status, bit_equal, close, column_mismatch, fixture_tags, load,
+                       load_params, parity_vs_reference, single_names)
 from noahmp_amd import cases, layout as L
 
 pytestmark = pytest.mark.gpu
@@ -37,13 +37,14 @@ DEV = "cuda:0"
 def engines(engine_lib):
     from noahmp_amd.engine import Engine
     from noahmp_amd.params import Params
-    P = Params.builtin("STAS", "USGS")
-    cache = {}
+    cache, tables = {}, {}
 
-    def get(options, precision=4, math="ref"):
-        key = (tuple(int(x) for x in options), precision, math)
+    def get(options, precision=4, math="ref", tags=("STAS", "USGS")):
+        key = (tuple(int(x) for x in options), precision, math, tuple(tags))
         if key not in cache:
-            cache[key] = Engine(P, dict(zip(L.OPTION_NAMES, key[0])), device=0,
+            if tags not in tables:
+                tables[tags] = Params.builtin(*tags)
+            cache[key] = Engine(tables[tags], dict(zip(L.OPTION_NAMES, key[0])), device=0,
                                 precision=precision, math=math)
         return cache[key]
     return get
@@ -72,7 +73,7 @@ def oracle_single(port, g, precision):
 @pytest.mark.parametrize("name", single_names())
 def test_single_call_vs_reference(engines, name):
     g = load(f"single_{name}.npz")
-    r, msg = parity_vs_reference(*run_single(engines(g["options"]), g), g)
+    r, msg = parity_vs_reference(*run_single(engines(g["options"], tags=fixture_tags(g)), g), g)
     print(name, r)
     assert not msg, f"{name}: {msg}"
 
@@ -83,7 +84,7 @@ def test_single_call_bit_exact_vs_reference(engines, name):
     (csrc/glibc_math.h), so the kernel must reproduce the reference Fortran
     bit for bit: every state field, every one of the 58 outputs, ISNOW, status."""
     g = load(f"single_{name}.npz")
-    st, isn, dg, status = run_single(engines(g["options"]), g)
+    st, isn, dg, status = run_single(engines(g["options"], tags=fixture_tags(g)), g)
     exact = bit_equal(st, g["state1"]).all(0) & bit_equal(dg, g["diag"]).all(0) & \
         (isn == g["isnow1"]) & (as_ref_status(status) == g["status"])
     _, rep_s = column_mismatch(st, g["state1"], 0, 0, STATE_NAMES)
@@ -169,6 +170,18 @@ def test_trajectory_snow_distribution(engines):
     for k, (st, isn, dg, status) in enumerate(out):
         ex = bit_equal(st, g["states"][k]).all(0) & (isn == g["isnows"][k]) & \
             bit_equal(dg, g["diags"][k]).all(0)
+        assert ex.all(), (k, ex.mean())
+
+
+def test_trajectory_option_combo(engines):
+    """48 steps under combo_a (dynamic vegetation + carbon, Jarvis canopy
+    resistance, Chen97 surface layer, ... -- tests/golden/make_golden.py):
+    bit-exact to the reference at every step."""
+    g = load("traj_combo_a.npz")
+    out = _trajectory(engines(g["options"]), g)
+    for k, (st, isn, dg, status) in enumerate(out):
+        ex = bit_equal(st, g["states"][k]).all(0) & (isn == g["isnows"][k]) & \
+            bit_equal(dg, g["diags"][k]).all(0) & (as_ref_status(status) == g["statuses"][k])
         assert ex.all(), (k, ex.mean())
 
 

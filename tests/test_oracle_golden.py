@@ -8,14 +8,15 @@ order, same libm, no contraction.
 import numpy as np
 import pytest
 
-from golden_io import as_ref_status, bit_equal, load, load_params, single_names
+from golden_io import (as_ref_status, bit_equal, fixture_params, fixture_tags, load, load_params,
+                       single_names)
 from noahmp_amd import layout as L
 
 
 @pytest.mark.parametrize("name", single_names())
 def test_single_call_bit_exact(oracle_port, name):
     g = load(f"single_{name}.npz")
-    P = load_params()
+    P = fixture_params(g)
     st, isn, dg, status = oracle_port.step(P, tuple(g["options"]), g["zsoil"], float(g["dt"]),
                                            int(g["yearlen"]), float(g["julian"]), g["state0"],
                                            g["isnow0"], g["static_f"], g["static_i"], g["forcing"])
@@ -27,7 +28,7 @@ def test_single_call_bit_exact(oracle_port, name):
     assert not bad.any(), [L.DIAG_FULL[f] for f in np.nonzero(bad.any(1))[0]]
 
 
-@pytest.mark.parametrize("name", ["casenml", "snow"])
+@pytest.mark.parametrize("name", ["casenml", "snow", "combo_a"])
 def test_trajectory_bit_exact(oracle_port, name):
     g = load(f"traj_{name}.npz")
     P = load_params()
@@ -64,6 +65,11 @@ def test_fixture_coverage():
     for k, name in enumerate(L.OPTION_NAMES):
         lo, hi = L.OPTION_RANGES[name]
         assert {o[k] for o in opts} == set(range(lo, hi + 1)), name
+    tags = {fixture_tags(load(f"single_{n}.npz")) for n in single_names()}
+    assert {("STAS", "USGS"), ("STAS-RUC", "USGS"), ("STAS", "MODIFIED_IGBP_MODIS_NOAH"),
+            ("STAS-RUC", "MODIFIED_IGBP_MODIS_NOAH")} <= tags
+    combos = [o for o in opts if sum(v != d for v, d in zip(o, L.options_tuple(L.CASE_NML_OPTIONS))) >= 3]
+    assert len(combos) >= 3, "option-combination fixtures"
     t = load("traj_snow.npz")
     assert (t["isnows"] != t["isnows"][:1]).any(), "snow trajectory never changes layering"
 
@@ -90,7 +96,7 @@ def test_cr_math_restatement_meets_parity_bar(oracle_port, name):
     is glibc float-libm rounding, not algorithm."""
     from golden_io import parity_vs_reference
     g = load(f"single_{name}.npz")
-    out = oracle_port.step(load_params(), tuple(g["options"]), g["zsoil"], float(g["dt"]),
+    out = oracle_port.step(fixture_params(g), tuple(g["options"]), g["zsoil"], float(g["dt"]),
                            int(g["yearlen"]), float(g["julian"]), g["state0"], g["isnow0"],
                            g["static_f"], g["static_i"], g["forcing"], precision="cr")
     r, msg = parity_vs_reference(*out, g)

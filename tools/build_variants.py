@@ -20,6 +20,12 @@ VARIANTS = {
     "b128": ("-DNMP_BLOCK=128",),
     "b64": ("-DNMP_BLOCK=64",),
     "b512": ("-DNMP_BLOCK=512",),
+    "k6": ("-DNMP_VEGE_K=6",),
+    "k10": ("-DNMP_VEGE_K=10",),
+    "k12": ("-DNMP_VEGE_K=12",),
+    "k20": ("-DNMP_VEGE_K=20",),
+    "k20lds": ("-DNMP_VEGE_K=20", "-DNMP_LDS_PAD=32768"),
+    "k12off": ("-DNMP_VEGE_K=12", "-DNMP_VPOOL_OFF"),
     "mlicm": ("-mllvm", "-disable-machine-licm=false"),
     "w4_mlicm": ("-DNMP_WAVES_PER_EU=4", "-mllvm", "-disable-machine-licm=false"),
 }
