@@ -87,6 +87,39 @@ DEV void esat(T t, T& esw, T& esi, T& desw, T& desi) {
 template <class T>
 DEV T tdc(T t) { return rmin(L(50.0), rmax(L(-50.0), (t - TFRZ))); }
 
+// The esat callers use (TT > 0) ? water : ice of each pair.  Evaluating only
+// that pair behind a real branch (same expressions as esat) halves the work
+// in waves whose lanes agree on the sign; mixed waves run both sides.
+template <class T>
+DEV void esat_sel(T t, T& es, T& des) {
+  if (t > L(0.0)) {
+    es = L(100.) * (L(6.107799961) + t * (L(4.436518521E-01) + t * (L(1.428945805E-02) +
+         t * (L(2.650648471E-04) + t * (L(3.031240396E-06) + t * (L(2.034080948E-08) +
+         t * L(6.136820929E-11)))))));
+    des = L(100.) * (L(4.438099984E-01) + t * (L(2.857002636E-02) + t * (L(7.938054040E-04) +
+          t * (L(1.215215065E-05) + t * (L(1.036561403E-07) + t * (L(3.532421810e-10) +
+          t * L(-7.090244804E-13)))))));
+  } else {
+    es = L(100.) * (L(6.109177956) + t * (L(5.034698970E-01) + t * (L(1.886013408E-02) +
+         t * (L(4.176223716E-04) + t * (L(5.824720280E-06) + t * (L(4.838803174E-08) +
+         t * L(1.838826904E-10)))))));
+    des = L(100.) * (L(5.030305237E-01) + t * (L(3.773255020E-02) + t * (L(1.267995369E-03) +
+          t * (L(2.477563108E-05) + t * (L(3.005693132E-07) + t * (L(2.158542548E-09) +
+          t * L(7.131097725E-12)))))));
+  }
+}
+// value only (the derivative unused)
+template <class T>
+DEV T esat_val(T t) {
+  if (t > L(0.0))
+    return L(100.) * (L(6.107799961) + t * (L(4.436518521E-01) + t * (L(1.428945805E-02) +
+           t * (L(2.650648471E-04) + t * (L(3.031240396E-06) + t * (L(2.034080948E-08) +
+           t * L(6.136820929E-11)))))));
+  return L(100.) * (L(6.109177956) + t * (L(5.034698970E-01) + t * (L(1.886013408E-02) +
+         t * (L(4.176223716E-04) + t * (L(5.824720280E-06) + t * (L(4.838803174E-08) +
+         t * L(1.838826904E-10)))))));
+}
+
 // tdfcnd: func.f90:1500-1595
 template <class T, bool R>
 DEV T tdfcnd(const SoilRec& S, T smc, T sh2o) {
@@ -449,28 +482,51 @@ DEV void ragrb(T sqrt_dleaf_uc, int iter, T vai, T rhoair, T hg, T tah, T zpd, T
 }
 
 // stomata (Ball-Berry bisection): func.f90:3739-3887
+// The sunlit and shaded calls (:2765-2770) share everything but APAR, so the
+// APAR-independent prelude (:3829-3845: CF, KC, KO, AWC, CP, VCMX, RLB) is
+// evaluated once (same expressions, bit-identical) and each call runs only
+// its bisection.
+template <class T>
+struct StomataPre {
+  T cf, kc, ko, awc, cp, vcmx, rlb;
+};
+
 template <class T, bool R>
-DEV void stomata(const VegRec& V, T igs, T sfcprs, T sfctmp, T apar, T tv, T ea, T ei, T o2,
-                 T co2, T foln, T btran, T rb, T& rs, T& psn) {
+DEV StomataPre<T> stomata_pre(const VegRec& V, bool any_light, T sfcprs, T sfctmp, T tv, T o2,
+                              T foln, T btran, T rb) {
+  typedef Mth<T, R> M;
+  StomataPre<T> p;
+  p.cf = sfcprs / (RGAS * sfctmp) * L(1.0e06);
+  p.kc = p.ko = p.awc = p.cp = p.vcmx = p.rlb = L(0.0);
+  if (any_light) {
+    T fnf = rmin(foln / rmax(MPE, (T)V.folnmx), L(1.0));
+    T tc = tv - TFRZ;
+    T ex = (tc - L(25.0)) / L(10.0);
+    p.kc = (T)V.kc25 * M::pow((T)V.akc, ex);
+    p.ko = (T)V.ko25 * M::pow((T)V.ako, ex);
+    p.awc = p.kc * (L(1.0) + o2 / p.ko);
+    p.cp = L(0.5) * p.kc / p.ko * o2 * L(0.21);
+    p.vcmx = (T)V.vcmx25 /
+             (L(1.0) + M::exp((L(-2.2E05) + L(710.0) * (tc + TFRZ)) / (L(8.314) * (tc + TFRZ)))) *
+             fnf * btran * (M::pow((T)V.avcmx, ex));
+    p.rlb = rb / p.cf;
+  }
+  return p;
+}
+
+template <class T, bool R>
+DEV void stomata_solve(const VegRec& V, const StomataPre<T>& p, T igs, T sfcprs, T apar, T ea,
+                       T ei, T co2, T& rs, T& psn) {
   typedef Mth<T, R> M;
   const T CIERR = L(5.0E-2);
-  T cf = sfcprs / (RGAS * sfctmp) * L(1.0e06);
+  const T cf = p.cf;
   rs = L(1.0) / (T)V.bp * cf;
   psn = L(0.0);
   if (apar <= L(0.0)) return;
-  T fnf = rmin(foln / rmax(MPE, (T)V.folnmx), L(1.0));
-  T tc = tv - TFRZ;
   T ppf = L(4.6) * apar;
   T j = ppf * (T)V.qe25;
-  T ex = (tc - L(25.0)) / L(10.0);
-  T kc = (T)V.kc25 * M::pow((T)V.akc, ex);
-  T ko = (T)V.ko25 * M::pow((T)V.ako, ex);
-  T awc = kc * (L(1.0) + o2 / ko);
-  T cp = L(0.5) * kc / ko * o2 * L(0.21);
-  T vcmx = (T)V.vcmx25 /
-           (L(1.0) + M::exp((L(-2.2E05) + L(710.0) * (tc + TFRZ)) / (L(8.314) * (tc + TFRZ)))) *
-           fnf * btran * (M::pow((T)V.avcmx, ex));
-  T rlb = rb / cf;
+  const T kc = p.kc, awc = p.awc, cp = p.cp, vcmx = p.vcmx, rlb = p.rlb;
+  (void)kc;
   T cihigh = L(1.5) * co2, cilow = L(0.0);
   const int c3c4 = V.c3c4;
   const T mp = (T)V.mp, bp = (T)V.bp;
@@ -1234,10 +1290,8 @@ DEV void sflx_column(const DevParams& P, const KArgs<T>& A, Col<T>& c, const Sin
     T vaie = rmin(L(6.0), vai / fveg);
     T laisune = rmin(L(6.0), laisun / fveg);
     T laishae = rmin(L(6.0), laisha / fveg);
-    T esatw, esati, dsatw, dsati;
     T tt = tdc(tgv);
-    esat(tt, esatw, esati, dsatw, dsati);
-    T estg = (tt > L(0.0)) ? esatw : esati;
+    T estg = esat_val(tt);
     c.qsfc = L(0.622) * eair / (c.psfc - L(0.378) * eair);
     T hcan = htop;
     // HCAN = HVT and Z0M = Z0MVT here: LOG(HCAN/Z0M) is veg-type-only
@@ -1269,15 +1323,15 @@ DEV void sflx_column(const DevParams& P, const KArgs<T>& A, Col<T>& c, const Sin
                   cwp, mpe, fhg, rahg, rb);
       T rawg = rahg;
       tt = tdc(c.tv);
-      esat(tt, esatw, esati, dsatw, dsati);
-      T estv = (tt > L(0.0)) ? esatw : esati;
-      T destv = (tt > L(0.0)) ? dsatw : dsati;
+      T estv, destv;
+      esat_sel(tt, estv, destv);
       if (iter == 1) {
         if (o.crs == 1) {
-          stomata<T, R>(V, igs, c.sfcprs, c.sfctmp, parsun, c.tv, c.eah, estv, c.o2air, c.co2air,
-                        c.foln, btran, rb, rssun, psnsun);
-          stomata<T, R>(V, igs, c.sfcprs, c.sfctmp, parsha, c.tv, c.eah, estv, c.o2air, c.co2air,
-                        c.foln, btran, rb, rssha, psnsha);
+          const StomataPre<T> sp =
+              stomata_pre<T, R>(V, parsun > L(0.0) || parsha > L(0.0), c.sfcprs, c.sfctmp, c.tv,
+                                c.o2air, c.foln, btran, rb);
+          stomata_solve<T, R>(V, sp, igs, c.sfcprs, parsun, c.eah, estv, c.co2air, rssun, psnsun);
+          stomata_solve<T, R>(V, sp, igs, c.sfcprs, parsha, c.eah, estv, c.co2air, rssha, psnsha);
         }
         if (o.crs == 2) {
           canres<T, R>(V, c.sfcprs, c.tv, parsun, c.eah, btran, rssun, psnsun);
@@ -1333,9 +1387,8 @@ DEV void sflx_column(const DevParams& P, const KArgs<T>& A, Col<T>& c, const Sin
 #pragma unroll 1
     for (int iter = 1; iter <= 5; ++iter) {
       tt = tdc(tgv);
-      esat(tt, esatw, esati, dsatw, dsati);
-      estg = (tt > L(0.0)) ? esatw : esati;
-      T destg = (tt > L(0.0)) ? dsatw : dsati;
+      T destg;
+      esat_sel(tt, estg, destg);
       irg = cir * p4(tgv) + air;
       shg = csh * (tgv - c.tah);
       evg = cev * (estg * rhsur - c.eah);
@@ -1383,7 +1436,10 @@ DEV void sflx_column(const DevParams& P, const KArgs<T>& A, Col<T>& c, const Sin
     T cir = emg * SB;
     T cgh = L(2.0) * df_top / dz_top;
     T z0h = z0mg, ehb = L(0.0), csh = L(0.0), cev = L(0.0), estg = L(0.0);
-    T esatw, esati, dsatw, dsati;
+    // saturation pressure at TGB: each iteration's closing value is the next
+    // iteration's opening value (same TGB), so it is carried, not recomputed
+    T es_tgb, des_tgb;
+    esat_sel(tdc(tgb), es_tgb, des_tgb);
     irb = shb = evb = ghb = L(0.0);
     const Sfc1Logs<T, R> lgb = (o.sfc == 1) ? Sfc1Logs<T, R>(zlvl, zpdg, z0mg, z0h, c.status)
                                             : Sfc1Logs<T, R>{};
@@ -1404,10 +1460,8 @@ DEV void sflx_column(const DevParams& P, const KArgs<T>& A, Col<T>& c, const Sin
       T rahb = rmax(L(1.0), L(1.0) / (chb * ur));
       T rawb = rahb;
       ehb = L(1.0) / rahb;
-      T tt = tdc(tgb);
-      esat(tt, esatw, esati, dsatw, dsati);
-      estg = (tt > L(0.0)) ? esatw : esati;
-      T destg = (tt > L(0.0)) ? dsatw : dsati;
+      estg = es_tgb;
+      const T destg = des_tgb;
       csh = rhoair * CPAIR / rahb;
       cev = rhoair * CPAIR / gammag / (rsurf + rawb);
       irb = cir * p4(tgb) - emg * c.lwdn;
@@ -1423,10 +1477,10 @@ DEV void sflx_column(const DevParams& P, const KArgs<T>& A, Col<T>& c, const Sin
       ghb = ghb + cgh * dtg;
       tgb = tgb + dtg;
       h = csh * (tgb - c.sfctmp);
-      tt = tdc(tgb);
-      esat(tt, esatw, esati, dsatw, dsati);
-      estg = (tt > L(0.0)) ? esatw : esati;
-      c.qsfc = L(0.622) * (estg * rhsur) / (c.psfc - L(0.378) * (estg * rhsur));
+      esat_sel(tdc(tgb), es_tgb, des_tgb);
+      estg = es_tgb;
+      // QSFC is overwritten every iteration and read only after the loop
+      if (iter == 5) c.qsfc = L(0.622) * (estg * rhsur) / (c.psfc - L(0.378) * (estg * rhsur));
     }
     if (o.stc == 1 && c.snowh > L(0.05) && tgb > TFRZ) {
       tgb = TFRZ;

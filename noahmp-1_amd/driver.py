@@ -30,7 +30,7 @@ import torch.distributed as dist
 
 from . import cases, layout as L, shard, timeman
 from .config import Config
-from .engine import ColumnState, Engine
+from .engine import ColumnState, Engine, StreamShards
 from .params import Params
 
 
@@ -63,13 +63,16 @@ def _is_boundary(t: datetime.datetime, t0: datetime.datetime, every) -> bool:
 class OfflineDriver:
     def __init__(self, cfg: Config, cols: cases.ColumnSet, device: int = 0,
                  params: Params | None = None, forcing=None, precision: int = 4,
-                 math: str = "ref", zsoil=cases.CASE_NML_ZSOIL, write: bool = True):
+                 math: str = "ref", zsoil=cases.CASE_NML_ZSOIL, write: bool = True,
+                 streams: int = 2):
         self.cfg = cfg
         self.engine = Engine(params or Params.builtin(), cfg.engine_options(), device, precision,
                              math)
         self.dtype = self.engine.dtype
         self.dev = torch.device("cuda", device)
         self.cs = ColumnState.from_host(cols, self.dev, self.dtype)
+        # column ranges on their own streams: launch tails overlap (engine.StreamShards)
+        self.ranges = StreamShards(self.engine, self.cs, streams)
         self.forcing = forcing or SyntheticForcing(cols)
         self.zsoil = [float(z) for z in zsoil]
         self.dt = cfg.timestep.total_seconds()
@@ -81,6 +84,7 @@ class OfflineDriver:
 
     # ---- restart -----------------------------------------------------------------
     def save_restart(self, path: str):
+        self.ranges.join()
         np.savez(path, time=np.array(self.t.isoformat()), step=np.int64(self.step_index),
                  state=self.cs.state.cpu().numpy(), isnow=self.cs.isnow.cpu().numpy(),
                  static_f=self.cs.static_f.cpu().numpy(), static_i=self.cs.static_i.cpu().numpy(),
@@ -88,6 +92,7 @@ class OfflineDriver:
                  layout=np.array(",".join(n for n, _ in L.STATE_FIELDS)))
 
     def load_restart(self, path: str):
+        self.ranges.join()  # no range may still be stepping the state being replaced
         with np.load(path, allow_pickle=False) as z:
             assert str(z["layout"]) == ",".join(n for n, _ in L.STATE_FIELDS), "state layout"
             for name in ("state", "isnow", "static_f", "static_i", "status"):
@@ -109,11 +114,13 @@ class OfflineDriver:
             t1 = t0 + cfg.timestep
             out = _is_boundary(t1, cfg.begdatetime, out_every)
             f = torch.as_tensor(self.forcing(self.step_index, t0), device=self.dev).to(self.dtype)
-            self.engine.step(self.cs, f, self.zsoil, self.dt, timeman.julian(t0),
-                             timeman.yearlen(t0.year), self.diag if out else None,
-                             L.DIAG_OUT_LEVEL if out else L.DIAG_NONE)
+            self.ranges.step(f, self.zsoil, self.dt, timeman.julian(t0), timeman.yearlen(t0.year),
+                             self.diag if out else None,
+                             L.DIAG_OUT_LEVEL if out else L.DIAG_NONE,
+                             after=torch.cuda.current_stream(self.dev))
             self.t, self.step_index = t1, self.step_index + 1
             if out and self.write:
+                self.ranges.join()
                 d = shard.gather_diag(self.diag) if dist.is_initialized() else self.diag
                 if rank == 0:
                     os.makedirs(cfg.outdir, exist_ok=True)
@@ -124,5 +131,6 @@ class OfflineDriver:
             if _is_boundary(t1, cfg.begdatetime, res_every) and self.write:
                 os.makedirs(cfg.resdir, exist_ok=True)
                 self.save_restart(os.path.join(cfg.resdir, f"RESTART.{_stamp(t1)}.r{rank}.npz"))
+        self.ranges.join()
         torch.cuda.synchronize(self.dev)
         return self

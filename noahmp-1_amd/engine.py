@@ -20,8 +20,9 @@ from .params import Params
 MATH_REF, MATH_FAST = 0, 1
 
 
-def _ptr(t):
-    return C.c_void_p(t.data_ptr()) if t is not None else C.c_void_p(0)
+def _ptr(t, off: int = 0):
+    """Device pointer of t, `off` elements in (a column offset into a field-major array)."""
+    return C.c_void_p(t.data_ptr() + off * t.element_size()) if t is not None else C.c_void_p(0)
 
 
 @dataclass
@@ -111,19 +112,26 @@ class Engine:
 
     def step(self, cs: ColumnState, forcing: torch.Tensor, zsoil, dt: float, julian: float,
              yearlen: int, diag: torch.Tensor | None = None, diag_level: int = L.DIAG_NONE,
-             stream=None):
-        """One noahmp_sflx step for every column (enqueued on `stream`)."""
+             stream=None, cols: tuple[int, int] | None = None):
+        """One noahmp_sflx step for every column (enqueued on `stream`).
+
+        cols=(lo, hi) steps only columns lo..hi-1, in place (pointer offsets with
+        ld = cs.ncol; forcing and diag are indexed by the same columns), so
+        column ranges can be stepped on different streams."""
         self._check_cols(cs, forcing)
         n = cs.ncol
+        lo, hi = (0, n) if cols is None else (int(cols[0]), int(cols[1]))
+        assert 0 <= lo <= hi <= n
         if diag_level != L.DIAG_NONE:
             nd = L.NDIAG_FULL if diag_level == L.DIAG_FULL_LEVEL else L.NDIAG_OUT
             assert diag is not None and diag.shape == (nd, n) and diag.dtype == self.dtype
         zs = (C.c_float * 4)(*[float(z) for z in zsoil])
         s = stream if stream is not None else torch.cuda.current_stream(self.device)
-        _lib.check(self._lib.nmp_step(self._h, n, n, zs, float(dt), float(julian), int(yearlen),
-                                      _ptr(cs.state), _ptr(cs.isnow), _ptr(cs.static_f),
-                                      _ptr(cs.static_i), _ptr(forcing), _ptr(diag), int(diag_level),
-                                      _ptr(cs.status), C.c_void_p(s.cuda_stream)), "nmp_step")
+        _lib.check(self._lib.nmp_step(self._h, hi - lo, n, zs, float(dt), float(julian),
+                                      int(yearlen), _ptr(cs.state, lo), _ptr(cs.isnow, lo),
+                                      _ptr(cs.static_f, lo), _ptr(cs.static_i, lo),
+                                      _ptr(forcing, lo), _ptr(diag, lo), int(diag_level),
+                                      _ptr(cs.status, lo), C.c_void_p(s.cuda_stream)), "nmp_step")
 
     def run(self, cs: ColumnState, forcings: torch.Tensor, zsoil, dt: float, julian0: float,
             yearlen: int, nsteps: int, diag: torch.Tensor | None = None,
@@ -160,3 +168,47 @@ class Engine:
                                          _ptr(diag), int(diag_level), int(out_every), int(slots),
                                          int(dstride), _ptr(cs.status),
                                          C.c_void_p(s.cuda_stream)), "nmp_run_out")
+
+
+class StreamShards:
+    """Steps one ColumnState as `nshards` column ranges, each on its own HIP stream.
+
+    Columns are independent and a range's step t+1 depends only on its own step
+    t, so the ranges' launches need no synchronisation with each other.  While
+    one range's launch drains its last waves, the other range's waves fill the
+    idle SIMDs, which hides the per-launch tail (DESIGN.md "Launch structure").
+    `join()` makes a stream wait for every range, and is needed before the
+    caller reads state or diagnostics."""
+
+    def __init__(self, engine: Engine, cs: ColumnState, nshards: int = 2, device=None):
+        n = cs.ncol
+        nshards = max(1, min(int(nshards), max(n, 1)))
+        self.engine, self.cs = engine, cs
+        dev = torch.device("cuda", engine.device) if device is None else torch.device(device)
+        self.streams = [torch.cuda.Stream(dev) for _ in range(nshards)]
+        self.ranges = [(n * i // nshards, n * (i + 1) // nshards) for i in range(nshards)]
+
+    def step(self, forcing: torch.Tensor, zsoil, dt: float, julian: float, yearlen: int,
+             diag: torch.Tensor | None = None, diag_level: int = L.DIAG_NONE, events=None,
+             after: torch.cuda.Stream | None = None):
+        """One step of every range.  `after`: a stream whose pending work (e.g. the
+        forcing upload) each range waits for first; tensors from it are kept alive
+        until the ranges are done with them.  events: per-range (start, end) pairs."""
+        for i, (st, rng) in enumerate(zip(self.streams, self.ranges)):
+            if after is not None:
+                st.wait_stream(after)
+                forcing.record_stream(st)
+                if diag is not None:
+                    diag.record_stream(st)
+            if events is not None:
+                events[i][0].record(st)
+            self.engine.step(self.cs, forcing, zsoil, dt, julian, yearlen, diag, diag_level,
+                             stream=st, cols=None if len(self.streams) == 1 else rng)
+            if events is not None:
+                events[i][1].record(st)
+
+    def join(self, stream: torch.cuda.Stream | None = None):
+        """Make `stream` (default: the current stream) wait for every range."""
+        s = stream if stream is not None else torch.cuda.current_stream(self.streams[0].device)
+        for st in self.streams:
+            s.wait_stream(st)

@@ -242,6 +242,39 @@ def test_run_out_ring_equals_repeated_step(engines):
         assert torch.equal(bits(ring[k]), bits(expect[k])), k
 
 
+@pytest.mark.parametrize("nshards", [2, 3])
+def test_stream_shards_equal_single_launch(engines, nshards):
+    """Column ranges on their own streams (engine.StreamShards, the bench and
+    driver default) == one launch per step, bitwise, over 6 steps with
+    diagnostics on alternate steps; 200,003 columns = ragged ranges."""
+    from noahmp_amd.engine import ColumnState, StreamShards
+    from noahmp_amd.params import Params
+    n = 200_003
+    eng = engines([L.CASE_NML_OPTIONS[k] for k in L.OPTION_NAMES])
+    cols = cases.make_columns(n, "mixed", Params.builtin().as_dict(), seed=6, julian=200.0)
+    F = [torch.as_tensor(cases.forcing_step(cols, 200.0 + s / 48.0, 365, s, seed=6), device=DEV)
+         for s in range(6)]
+    a = ColumnState.from_host(cols, DEV)
+    b = ColumnState.from_host(cols, DEV)
+    sh = StreamShards(eng, a, nshards)
+    da = [torch.zeros((L.NDIAG_OUT, n), device=DEV) for _ in range(3)]
+    db = [torch.zeros((L.NDIAG_OUT, n), device=DEV) for _ in range(3)]
+    for s in range(6):
+        out = s % 2 == 1
+        lvl = L.DIAG_OUT_LEVEL if out else L.DIAG_NONE
+        sh.step(F[s], cases.CASE_NML_ZSOIL, 1800.0, 200.0 + s / 48.0, 365,
+                da[s // 2] if out else None, lvl)
+        eng.step(b, F[s], cases.CASE_NML_ZSOIL, 1800.0, 200.0 + s / 48.0, 365,
+                 db[s // 2] if out else None, lvl)
+    sh.join()
+    torch.cuda.synchronize()
+    bits = lambda t: t.view(torch.int32)
+    assert torch.equal(bits(a.state), bits(b.state)) and torch.equal(a.isnow, b.isnow)
+    assert torch.equal(a.status, b.status)
+    for x, y in zip(da, db):
+        assert torch.equal(bits(x), bits(y))
+
+
 def test_diag_levels_consistent(engines):
     """DIAG_OUT fields are the DIAG_FULL values (T2M = the fveg blend of T2MV/T2MB)."""
     from noahmp_amd.engine import ColumnState
