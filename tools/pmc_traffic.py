@@ -7,7 +7,8 @@ write-correction, where the corrections come from the calibration copy
 uncalibrated for non-16B accesses; calibrate on your own pattern).
 FETCH_SIZE/WRITE_SIZE are reported in KB (1024 B) by rocprofv3.
 
-usage: python tools/pmc_traffic.py gpurun_out/<tag> [--ncol N]
+usage: python tools/pmc_traffic.py gpurun_out/<tag> [--ncol N] [--streams S]
+(S = the bench's --streams: each dispatch covers ncol/S columns)
 """
 import csv
 import glob
@@ -49,6 +50,10 @@ def main():
     ncol = 1 << 20
     if "--ncol" in sys.argv:
         ncol = int(sys.argv[sys.argv.index("--ncol") + 1])
+    streams = 2
+    if "--streams" in sys.argv:
+        streams = int(sys.argv[sys.argv.index("--streams") + 1])
+    cols_per_launch = ncol / streams
     calib_n, nf = 4194304, 56
     cal_bytes = nf * calib_n * 4
     cf, _ = mean_for(os.path.join(base, "calib_FETCH_SIZE"), "FETCH_SIZE", "calib_soa_copy")
@@ -62,10 +67,11 @@ def main():
     sys.path.insert(0, ROOT)
     import noahmp_pkg  # noqa: F401
     from noahmp_amd import build
-    res = {"source_hash": build.source_hash(), "ncol": ncol, "precision": 4, "math": "ref", "kernel": KERNEL, "dispatches": nb,
+    res = {"source_hash": build.source_hash(), "ncol": ncol, "streams": streams,
+           "precision": 4, "math": "ref", "kernel": KERNEL, "dispatches": nb,
            "fetch_size_kb": bf, "write_size_kb": bw, "read_correction": rf,
            "write_correction": rw, "read_bytes": rd, "write_bytes": wr,
-           "bytes_per_launch": rd + wr, "bytes_per_colstep": (rd + wr) / ncol,
+           "bytes_per_launch": rd + wr, "bytes_per_colstep": (rd + wr) / cols_per_launch,
            "source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes ({base})"}
     sq = os.path.join(base, "bench_SQ")
     if os.path.isdir(sq):
