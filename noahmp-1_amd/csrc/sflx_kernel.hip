@@ -2717,10 +2717,12 @@ DEV void sflx_column(const DevParams& P, const KArgs<T>& A, Col<T>& c, const Sin
 
 // ---------------------------------------------------------------------------
 template <class T, bool R>
-// Occupancy target: 3 waves/SIMD for fp32 (168 VGPRs; measured faster than
-// 1-2 waves with fewer spills and than 4 waves; tools/sweep.sh), 1 for fp64.
+// Occupancy target: 4 waves/SIMD for fp32 (128 VGPRs), 1 for fp64.  With the
+// launch tails overlapped by two stream ranges (engine.StreamShards) 4 waves
+// measured 1,175 Mcs/s against 1,131 at 3 (168 VGPRs, fewer spills), 921 at 2
+// and 930 at 5 (tools/sweep.sh; DESIGN.md "Occupancy").
 #ifndef NMP_WAVES_PER_EU
-#define NMP_WAVES_PER_EU 3
+#define NMP_WAVES_PER_EU 4
 #endif
 #ifndef NMP_BLOCK
 #define NMP_BLOCK 256

@@ -26,6 +26,9 @@ VARIANTS = {
     "k20": ("-DNMP_VEGE_K=20",),
     "k20lds": ("-DNMP_VEGE_K=20", "-DNMP_LDS_PAD=32768"),
     "k12off": ("-DNMP_VEGE_K=12", "-DNMP_VPOOL_OFF"),
+    "w4_b128": ("-DNMP_WAVES_PER_EU=4", "-DNMP_BLOCK=128"),
+    "w4_b64": ("-DNMP_WAVES_PER_EU=4", "-DNMP_BLOCK=64"),
+    "w5": ("-DNMP_WAVES_PER_EU=5",),
     "mlicm": ("-mllvm", "-disable-machine-licm=false"),
     "w4_mlicm": ("-DNMP_WAVES_PER_EU=4", "-mllvm", "-disable-machine-licm=false"),
 }
