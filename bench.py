@@ -33,6 +33,10 @@ import noahmp_pkg  # noqa: E402,F401
 from noahmp_amd import cases, layout as L, shard  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E, /opt/skills/guides/MI355X_MICROARCH.md
+# VALU issue peak: 256 CUs x 4 SIMD-32 x 2.4 GHz / 2 cycles per wave64 instruction
+# (MI355X_MICROARCH.md, "Wave scheduling"; f64 and transcendental instructions take
+# longer, so the fraction below is a lower bound on the VALU pipe's busy share)
+VALU_PEAK_GINST = 256 * 4 * 2.4 / 2
 METRIC = BASELINE_METRIC = "land-columns·timesteps/sec at 4 soil + 3 snow layers, 1/2/4/8 MI355X"
 
 
@@ -189,16 +193,25 @@ def main():
         bpl = bps / len(ranges.ranges)
         # the S launches of a step run concurrently: rate = bytes per step / GPU time per step
         achieved = bps / (step_ms * 1e-3) / 1e9
-        traffic = None
+        traffic = valu = None
         if os.path.exists(a.traffic):
             with open(a.traffic) as f:
                 tj = json.load(f)
             from noahmp_amd import build as _build
             if tj.get("ncol") == n and tj.get("precision") == a.precision and \
                     tj.get("streams", 1) == len(ranges.ranges) and \
-                    tj.get("math") == a.math and tj.get("source_hash") == _build.source_hash() \
+                    tj.get("math") == a.math and tj.get("kind", "mixed") == a.kind and \
+                    tj.get("source_hash") == _build.source_hash() \
                     and os.environ.get("NOAHMP_ENGINE_LIB") is None:
                 traffic = tj.get("bytes_per_launch")
+                if tj.get("SQ_INSTS_VALU"):
+                    # PMC wave-instructions per launch x launches per step / GPU time per step
+                    g = tj["SQ_INSTS_VALU"] * len(ranges.ranges) / (step_ms * 1e-3) / 1e9
+                    valu = {"achieved": g, "peak": VALU_PEAK_GINST, "unit": "G wave-instr/s",
+                            "frac": g / VALU_PEAK_GINST,
+                            "insts_per_wave": tj["SQ_INSTS_VALU"] / tj["SQ_WAVES"],
+                            "source": "SQ_INSTS_VALU / SQ_WAVES, rocprofv3 --pmc "
+                                      "(profiles/traffic.json)"}
         line = {
             "metric": METRIC, "value": value, "unit": "column-steps/s", "n_gpus": world,
             "steps": a.steps, "warmup": a.warmup, "ms_per_step": elapsed * 1e3 / a.steps,
@@ -218,7 +231,7 @@ def main():
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": "sflx_step_kernel", "kernel_ms": kern_ms,
                          "bytes_per_launch": bpl, "launches_per_step": len(ranges.ranges),
-                         "step_ms": step_ms, "bytes_per_step": bps},
+                         "step_ms": step_ms, "bytes_per_step": bps, "valu": valu},
             "cpu_baseline": cpu,
             "checks": {"status_nonzero_cols": st_bad, "stc_finite": finite},
         }

@@ -66,6 +66,13 @@ def main():
     for k in range(5):
         m, mx = w[..., k].mean(), w[..., k].max(1).mean()
         print(f"  {NAMES[k]:22s} {m:8.2f} {mx:8.2f}   {m / mx if mx else 0:.2f}")
+    v = tot[:, 0] if a.steps == 1 else None
+    h = np.bincount(buf[:, 0], minlength=21)
+    print("vege_flux trip histogram (last step):", h.tolist())
+    for K in (6, 7, 8, 10, 12):
+        frac = float((buf[:, 0] > K).mean())
+        wmax = np.minimum(buf[: a.ncol // 64 * 64, 0].reshape(-1, 64), K).max(1).mean()
+        print(f"  cap {K:2d}: columns over cap {100 * frac:5.2f} %  capped wave-max {wmax:.2f}")
 
 
 if __name__ == "__main__":

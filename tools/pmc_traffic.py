@@ -53,6 +53,9 @@ def main():
     streams = 2
     if "--streams" in sys.argv:
         streams = int(sys.argv[sys.argv.index("--streams") + 1])
+    kind = "mixed"
+    if "--kind" in sys.argv:
+        kind = sys.argv[sys.argv.index("--kind") + 1]
     cols_per_launch = ncol / streams
     calib_n, nf = 4194304, 56
     cal_bytes = nf * calib_n * 4
@@ -67,7 +70,7 @@ def main():
     sys.path.insert(0, ROOT)
     import noahmp_pkg  # noqa: F401
     from noahmp_amd import build
-    res = {"source_hash": build.source_hash(), "ncol": ncol, "streams": streams,
+    res = {"source_hash": build.source_hash(), "ncol": ncol, "streams": streams, "kind": kind,
            "precision": 4, "math": "ref", "kernel": KERNEL, "dispatches": nb,
            "fetch_size_kb": bf, "write_size_kb": bw, "read_correction": rf,
            "write_correction": rw, "read_bytes": rd, "write_bytes": wr,
