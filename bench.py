@@ -201,6 +201,7 @@ def main():
             if tj.get("ncol") == n and tj.get("precision") == a.precision and \
                     tj.get("streams", 1) == len(ranges.ranges) and \
                     tj.get("math") == a.math and tj.get("kind", "mixed") == a.kind and \
+                    tj.get("order", "as-generated") == a.order and \
                     tj.get("source_hash") == _build.source_hash() \
                     and os.environ.get("NOAHMP_ENGINE_LIB") is None:
                 traffic = tj.get("bytes_per_launch")
