@@ -18,6 +18,8 @@
  *                             = noahmp_sflx over every column core/module_noahmp_func.f90:66-476
  * nmp_run, nmp_run_out        the offline time loop around noahmp_run (run/main.py:12-14
  *                             stops after the namelist): many steps, one launch
+ * nmp_sflx_columns,           noahmp_sflx itself, argument for argument, on n host records
+ *   nmp_sflx_column                                         core/module_noahmp_func.f90:66-476
  * nmp_state_from_aos          layout bridge from noahmp_state_t records
  *                                                           core/module_noahmp_type.f90:10-42
  * nmp_finalize, nmp_strerror  (error path of utils `assert`/`stop`, core/module_noahmp_utils.f90:21-53)
@@ -50,7 +52,7 @@
 extern "C" {
 #endif
 
-#define NMP_ABI_VERSION 2
+#define NMP_ABI_VERSION 3
 
 /* ---- dimensions (core/module_noahmp_global.f90:9-13) -------------------- */
 #define NMP_NSOIL 4
@@ -169,6 +171,45 @@ enum {
   NMP_ST_STOP = 128   /* FIRE|ZLVL as the reference oracle reports them (one message) */
 };
 
+/* ---- one column, the reference calling sequence ---------------------------
+ * All 131 noahmp_sflx dummy arguments (core/module_noahmp_func.f90:66-91), in
+ * dummy-argument order.  Every member is 4 bytes and there is no padding, so a
+ * Fortran `type, bind(C)` with the same components in the same order maps onto
+ * it 1:1.  Arrays follow the reference bounds in C order:
+ * stc/zsnso[k] = Fortran (k-2), ficeold/snice/snliq[j] = (j-2),
+ * zsoil/soilwat/smc[k] = (k+1). */
+typedef struct nmp_sflx_args {
+  /* IN: time/space (:67) */
+  int32_t iloc, jloc;
+  float lat;
+  int32_t yearlen;
+  float julian, cosz;
+  /* IN: model configuration (:68) */
+  float dt, dx, dz8w;
+  int32_t nsoil;
+  float zsoil[NMP_NSOIL];
+  int32_t nsnow;
+  /* IN: vegetation / soil characteristics (:69-70) and the unused IZ0TLND (:71) */
+  float shdfac, shdmax;
+  int32_t slptyp, sltyp, lutyp, ice, ist, isc, iz0tlnd;
+  /* IN: forcing (:72-74) */
+  float sfctmp, sfcprs, psfc, uu, vv, q2, qc, soldn, lwdn, prcp, tbot, co2air, o2air, foln;
+  float ficeold[NMP_NSNOW];
+  float pblh, zlvl;
+  /* IN/OUT (:75-80) */
+  float albold, sneqvo;
+  float stc[NMP_NLAYER], soilwat[NMP_NSOIL], smc[NMP_NSOIL];
+  float tah, eah, fwet, canliq, canice, tv, tg, qsfc, qsnow;
+  int32_t isnow;
+  float zsnso[NMP_NLAYER], snowh, sneqv, snice[NMP_NSNOW], snliq[NMP_NSNOW];
+  float zwt, wa, wt, wslake, lfmass, rtmass, stmass, wood, stblcp, fastcp, lai, sai;
+  float cm, ch, tauss;
+  /* OUT (:82-91): the 58 intent(out) arguments, indexed by NMP_D_* */
+  float out[NMP_NDIAG_FULL];
+  /* OUT: NMP_ST_* bits of this call (what wrf_error_fatal / wrf_message reported) */
+  int32_t status;
+} nmp_sflx_args;
+
 /* ---- errors -------------------------------------------------------------- */
 enum {
   NMP_OK = 0,
@@ -234,10 +275,27 @@ int nmp_run_out(nmp_engine* eng, int64_t ncol, int64_t ld, const float zsoil[4],
 int nmp_state_from_aos(const void* records, int64_t n, int64_t ld, float* state, int32_t* isnow,
                        int32_t* static_i);
 
-/* Transcendental policy for fp32 engines: 0 = evaluate exp/log/pow/... in fp64
- * and round once (reproduces the glibc-compiled reference except at rare
- * rounding ties; default), 1 = ocml fp32 functions (faster, <= ~2 ulp).
- * Default can also be set with NMP_MATH=fast in the environment. */
+/* noahmp_sflx with the reference calling sequence (func.f90:66-91), for n
+ * HOST records: the records are packed into the SoA layout, stepped on the
+ * engine's GPU by the same kernel as nmp_step (all 58 outputs), and unpacked
+ * in place; synchronous.  Replaces a loop of `call noahmp_sflx(...)` over n
+ * columns (the per-column entry SURVEY 8b names nmp_sflx_column).
+ *  - nsoil must be 4 and nsnow 3; dt, julian, yearlen and zsoil must be the
+ *    same in every record of one call (they are launch-wide), else NMP_E_ARG.
+ *  - FICEOLD: the engine derives it from SNICE/SNLIQ at step start, as the
+ *    offline and WRF drivers compute it; a record whose FICEOLD of an active
+ *    snow layer differs from SNICE/(SNICE+SNLIQ) is rejected (NMP_E_ARG).
+ *  - iloc, jloc, dx, dz8w, qc, pblh and iz0tlnd never enter the arithmetic
+ *    (SURVEY H9); zlvl is intent(inout) but never modified, as in the reference.
+ *  - status receives the column's NMP_ST_* bits (0 = the reference would not
+ *    have called wrf_error_fatal / wrf_message). */
+int nmp_sflx_columns(nmp_engine* eng, nmp_sflx_args* cols, int64_t n);
+int nmp_sflx_column(nmp_engine* eng, nmp_sflx_args* col);
+
+/* Transcendental policy for fp32 engines: 0 = "ref", a bit-exact restatement of
+ * the glibc float libm the reference is linked against (csrc/glibc_math.h;
+ * default), 1 = ocml fp32 functions (faster, within a few ulp).  fp64 engines
+ * always use ocml double.  Default can also be set with NMP_MATH=fast. */
 int nmp_set_math(nmp_engine* eng, int mode);
 
 int nmp_engine_info(const nmp_engine* eng, int* device, int* precision, nmp_options* opts);

@@ -12,6 +12,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <new>
+#include <vector>
 
 #include "dev_params.h"
 #include "noahmp_engine.h"
@@ -293,6 +294,147 @@ int nmp_state_from_aos(const void* records, int64_t n, int64_t ld, float* state,
   }
   return NMP_OK;
 }
+
+}  // extern "C"
+
+namespace {
+
+// One record <-> column c of the SoA host arrays (field f at f*n + c).
+template <class T>
+struct SflxPack {
+  int64_t n;
+  std::vector<T> st, sf, fc, dg;
+  std::vector<int32_t> isn, si, status;
+  explicit SflxPack(int64_t n_)
+      : n(n_), st(NMP_NSTATE * n_), sf(NMP_NSTATIC_F * n_), fc(NMP_NFORCING * n_),
+        dg(NMP_NDIAG_FULL * n_), isn(n_), si(NMP_NSTATIC_I * n_), status(n_, 0) {}
+  T& S(int f, int64_t c) { return st[f * n + c]; }
+
+  void pack(const nmp_sflx_args& r, int64_t c) {
+    for (int k = 0; k < NMP_NLAYER; ++k) {
+      S(NMP_S_STC + k, c) = r.stc[k];
+      S(NMP_S_ZSNSO + k, c) = r.zsnso[k];
+    }
+    for (int j = 0; j < NMP_NSNOW; ++j) {
+      S(NMP_S_SNICE + j, c) = r.snice[j];
+      S(NMP_S_SNLIQ + j, c) = r.snliq[j];
+    }
+    for (int k = 0; k < NMP_NSOIL; ++k) {
+      S(NMP_S_SH2O + k, c) = r.soilwat[k];
+      S(NMP_S_SMC + k, c) = r.smc[k];
+    }
+    const float sc[] = {r.tv,     r.tg,    r.tah,    r.eah,    r.fwet,   r.canliq, r.canice,
+                        r.qsfc,   r.snowh, r.sneqv,  r.sneqvo, r.albold, r.tauss,  r.qsnow,
+                        r.zwt,    r.wa,    r.wt,     r.wslake, r.lai,    r.sai,    r.lfmass,
+                        r.rtmass, r.stmass, r.wood,  r.stblcp, r.fastcp, r.cm,     r.ch};
+    for (int i = 0; i < NMP_NSTATE - NMP_S_TV; ++i) S(NMP_S_TV + i, c) = sc[i];
+    isn[c] = r.isnow;
+    const float f[] = {r.lat, r.zlvl, r.shdfac, r.shdmax, r.tbot, r.foln};
+    for (int i = 0; i < NMP_NSTATIC_F; ++i) sf[i * n + c] = f[i];
+    const int32_t g[] = {r.lutyp, r.sltyp, r.slptyp, r.isc, r.ist, r.ice};
+    for (int i = 0; i < NMP_NSTATIC_I; ++i) si[i * n + c] = g[i];
+    const float a[] = {r.sfctmp, r.sfcprs, r.psfc, r.uu,   r.vv,     r.q2,
+                       r.soldn,  r.lwdn,   r.prcp, r.cosz, r.co2air, r.o2air};
+    for (int i = 0; i < NMP_NFORCING; ++i) fc[i * n + c] = a[i];
+  }
+
+  void unpack(nmp_sflx_args& r, int64_t c) {
+    for (int k = 0; k < NMP_NLAYER; ++k) {
+      r.stc[k] = (float)S(NMP_S_STC + k, c);
+      r.zsnso[k] = (float)S(NMP_S_ZSNSO + k, c);
+    }
+    for (int j = 0; j < NMP_NSNOW; ++j) {
+      r.snice[j] = (float)S(NMP_S_SNICE + j, c);
+      r.snliq[j] = (float)S(NMP_S_SNLIQ + j, c);
+    }
+    for (int k = 0; k < NMP_NSOIL; ++k) {
+      r.soilwat[k] = (float)S(NMP_S_SH2O + k, c);
+      r.smc[k] = (float)S(NMP_S_SMC + k, c);
+    }
+    float* sc[] = {&r.tv,     &r.tg,     &r.tah,    &r.eah,    &r.fwet,   &r.canliq, &r.canice,
+                   &r.qsfc,   &r.snowh,  &r.sneqv,  &r.sneqvo, &r.albold, &r.tauss,  &r.qsnow,
+                   &r.zwt,    &r.wa,     &r.wt,     &r.wslake, &r.lai,    &r.sai,    &r.lfmass,
+                   &r.rtmass, &r.stmass, &r.wood,   &r.stblcp, &r.fastcp, &r.cm,     &r.ch};
+    for (int i = 0; i < NMP_NSTATE - NMP_S_TV; ++i) *sc[i] = (float)S(NMP_S_TV + i, c);
+    r.isnow = isn[c];
+    for (int d = 0; d < NMP_NDIAG_FULL; ++d) r.out[d] = (float)dg[d * n + c];
+    r.status = status[c];
+  }
+};
+static_assert(NMP_NSTATE - NMP_S_TV == 28, "scalar state block");
+
+bool same_f(float a, float b) { return std::memcmp(&a, &b, sizeof(float)) == 0; }
+
+template <class T>
+int sflx_columns(nmp_engine* eng, nmp_sflx_args* cols, int64_t n) {
+  const nmp_sflx_args& r0 = cols[0];
+  for (int64_t c = 0; c < n; ++c) {
+    const nmp_sflx_args& r = cols[c];
+    if (r.nsoil != NMP_NSOIL || r.nsnow != NMP_NSNOW) return NMP_E_ARG;
+    if (r.isnow < -NMP_NSNOW || r.isnow > 0) return NMP_E_ARG;
+    if (!same_f(r.dt, r0.dt) || !same_f(r.julian, r0.julian) || r.yearlen != r0.yearlen)
+      return NMP_E_ARG;
+    for (int k = 0; k < NMP_NSOIL; ++k)
+      if (!same_f(r.zsoil[k], r0.zsoil[k])) return NMP_E_ARG;
+    // FICEOLD of the active snow layers must be the step-start ice fraction the
+    // engine derives (func.f90:5655 reads only those before a new layer exists)
+    for (int j = r.isnow + 3; j < NMP_NSNOW; ++j)
+      if (!same_f(r.ficeold[j], r.snice[j] / (r.snice[j] + r.snliq[j]))) return NMP_E_ARG;
+  }
+  SflxPack<T> h(n);
+  for (int64_t c = 0; c < n; ++c) h.pack(cols[c], c);
+  const size_t nb_st = h.st.size() * sizeof(T), nb_sf = h.sf.size() * sizeof(T),
+               nb_fc = h.fc.size() * sizeof(T), nb_dg = h.dg.size() * sizeof(T),
+               nb_i = (size_t)n * sizeof(int32_t);
+  const size_t total = nb_st + nb_sf + nb_fc + nb_dg + nb_i * (2 + NMP_NSTATIC_I);
+  char* d = nullptr;
+  if (hipMalloc(&d, total) != hipSuccess) return NMP_E_DEVICE;
+  char* p = d;
+  auto take = [&](size_t nb) { char* q = p; p += nb; return q; };
+  T* d_st = reinterpret_cast<T*>(take(nb_st));
+  T* d_sf = reinterpret_cast<T*>(take(nb_sf));
+  T* d_fc = reinterpret_cast<T*>(take(nb_fc));
+  T* d_dg = reinterpret_cast<T*>(take(nb_dg));
+  int32_t* d_isn = reinterpret_cast<int32_t*>(take(nb_i));
+  int32_t* d_status = reinterpret_cast<int32_t*>(take(nb_i));
+  int32_t* d_si = reinterpret_cast<int32_t*>(take(nb_i * NMP_NSTATIC_I));
+  int rc = NMP_OK;
+  if (hipMemcpy(d_st, h.st.data(), nb_st, hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(d_sf, h.sf.data(), nb_sf, hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(d_fc, h.fc.data(), nb_fc, hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(d_isn, h.isn.data(), nb_i, hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(d_si, h.si.data(), nb_i * NMP_NSTATIC_I, hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemset(d_status, 0, nb_i) != hipSuccess || hipMemset(d_dg, 0, nb_dg) != hipSuccess)
+    rc = NMP_E_DEVICE;
+  if (rc == NMP_OK)
+    rc = launch(eng, n, n, r0.zsoil, r0.dt, r0.julian, r0.yearlen, d_st, d_isn, d_sf, d_si, d_fc,
+                d_dg, NMP_DIAG_FULL, d_status, nullptr);
+  if (rc == NMP_OK && (hipDeviceSynchronize() != hipSuccess ||
+                       hipMemcpy(h.st.data(), d_st, nb_st, hipMemcpyDeviceToHost) != hipSuccess ||
+                       hipMemcpy(h.dg.data(), d_dg, nb_dg, hipMemcpyDeviceToHost) != hipSuccess ||
+                       hipMemcpy(h.isn.data(), d_isn, nb_i, hipMemcpyDeviceToHost) != hipSuccess ||
+                       hipMemcpy(h.status.data(), d_status, nb_i, hipMemcpyDeviceToHost) !=
+                           hipSuccess))
+    rc = NMP_E_DEVICE;
+  hipFree(d);
+  if (rc != NMP_OK) return rc;
+  for (int64_t c = 0; c < n; ++c) h.unpack(cols[c], c);
+  return NMP_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int nmp_sflx_columns(nmp_engine* eng, nmp_sflx_args* cols, int64_t n) {
+  if (!eng || n < 0 || (n > 0 && !cols)) return NMP_E_ARG;
+  if (n == 0) return NMP_OK;
+  if (ensure_device(eng->device) != NMP_OK) return NMP_E_DEVICE;
+  return eng->precision == 4 ? sflx_columns<float>(eng, cols, n)
+                             : sflx_columns<double>(eng, cols, n);
+}
+
+int nmp_sflx_column(nmp_engine* eng, nmp_sflx_args* col) { return nmp_sflx_columns(eng, col, 1); }
 
 void nmp_finalize(nmp_engine* eng) {
   if (!eng) return;

@@ -133,6 +133,15 @@ class Engine:
                                       _ptr(forcing, lo), _ptr(diag, lo), int(diag_level),
                                       _ptr(cs.status, lo), C.c_void_p(s.cuda_stream)), "nmp_step")
 
+    def sflx_columns(self, rec: np.ndarray) -> np.ndarray:
+        """noahmp_sflx with the reference calling sequence on host records
+        (layout.sflx_args_dtype(); nmp_sflx_columns), updated in place and returned.
+        Synchronous: packs, steps on the engine's GPU, unpacks."""
+        assert rec.dtype == L.sflx_args_dtype() and rec.flags.c_contiguous and rec.ndim == 1
+        _lib.check(self._lib.nmp_sflx_columns(self._h, C.c_void_p(rec.ctypes.data),
+                                              int(rec.shape[0])), "nmp_sflx_columns")
+        return rec
+
     def run(self, cs: ColumnState, forcings: torch.Tensor, zsoil, dt: float, julian0: float,
             yearlen: int, nsteps: int, diag: torch.Tensor | None = None,
             diag_level: int = L.DIAG_NONE, stream=None, out_every: int | None = None):

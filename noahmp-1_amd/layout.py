@@ -53,6 +53,80 @@ OPTION_RANGES = dict(opt_veg=(1, 5), opt_crs=(1, 2), opt_btr=(1, 3), opt_run=(1,
                      opt_alb=(1, 2), opt_snf=(1, 3), opt_tbot=(1, 2), opt_stc=(1, 2))
 
 
+# struct nmp_sflx_args: the 131 noahmp_sflx dummy arguments in dummy order
+# (core/module_noahmp_func.f90:66-91) + the status word; (name, "i"|"f", count)
+SFLX_ARGS = (
+    [("iloc", "i", 1), ("jloc", "i", 1), ("lat", "f", 1), ("yearlen", "i", 1),
+     ("julian", "f", 1), ("cosz", "f", 1), ("dt", "f", 1), ("dx", "f", 1), ("dz8w", "f", 1),
+     ("nsoil", "i", 1), ("zsoil", "f", NSOIL), ("nsnow", "i", 1), ("shdfac", "f", 1),
+     ("shdmax", "f", 1)]
+    + [(n, "i", 1) for n in ("slptyp", "sltyp", "lutyp", "ice", "ist", "isc", "iz0tlnd")]
+    + [(n, "f", 1) for n in ("sfctmp", "sfcprs", "psfc", "uu", "vv", "q2", "qc", "soldn", "lwdn",
+                             "prcp", "tbot", "co2air", "o2air", "foln")]
+    + [("ficeold", "f", NSNOW), ("pblh", "f", 1), ("zlvl", "f", 1), ("albold", "f", 1),
+       ("sneqvo", "f", 1), ("stc", "f", NLAYER), ("soilwat", "f", NSOIL), ("smc", "f", NSOIL)]
+    + [(n, "f", 1) for n in ("tah", "eah", "fwet", "canliq", "canice", "tv", "tg", "qsfc",
+                             "qsnow")]
+    + [("isnow", "i", 1), ("zsnso", "f", NLAYER), ("snowh", "f", 1), ("sneqv", "f", 1),
+       ("snice", "f", NSNOW), ("snliq", "f", NSNOW)]
+    + [(n, "f", 1) for n in ("zwt", "wa", "wt", "wslake", "lfmass", "rtmass", "stmass", "wood",
+                             "stblcp", "fastcp", "lai", "sai", "cm", "ch", "tauss")]
+    + [("out", "f", 58), ("status", "i", 1)]
+)
+
+
+def sflx_args_dtype():
+    """numpy structured dtype with the byte layout of struct nmp_sflx_args."""
+    import numpy as np
+    return np.dtype([(n, np.int32 if k == "i" else np.float32) if w == 1 else
+                     (n, np.int32 if k == "i" else np.float32, (w,)) for n, k, w in SFLX_ARGS])
+
+
+_REC_STATE = {"SH2O": "soilwat"}
+_REC_STATIC_I = {"VEGTYP": "lutyp", "SOILTYP": "sltyp", "SLOPETYP": "slptyp",
+                 "SOILCOLOR": "isc", "IST": "ist", "ICE": "ice"}
+
+
+def sflx_records(state, isnow, static_f, static_i, forcing, zsoil, dt, julian, yearlen):
+    """nmp_sflx_args records (host) from field-major SoA arrays (n columns):
+    the reference calling sequence of the same step, FICEOLD derived from
+    SNICE/SNLIQ as the offline and WRF drivers do."""
+    import numpy as np
+    n = int(np.shape(isnow)[0])
+    r = np.zeros(n, sflx_args_dtype())
+    r["nsoil"], r["nsnow"], r["yearlen"] = NSOIL, NSNOW, int(yearlen)
+    r["dt"], r["julian"] = np.float32(dt), np.float32(julian)
+    r["zsoil"] = np.asarray(zsoil, np.float32)[None, :]
+    for name, w in STATE_FIELDS:
+        o = STATE_OFF[name][0]
+        key = _REC_STATE.get(name, name.lower())
+        r[key] = state[o:o + w].T if w > 1 else state[o]
+    r["isnow"] = isnow
+    for i, name in enumerate(STATIC_F):
+        r[name.lower()] = static_f[i]
+    for i, name in enumerate(STATIC_I):
+        r[_REC_STATIC_I[name]] = static_i[i]
+    for i, name in enumerate(FORCING):
+        r[name.lower()] = forcing[i]
+    with np.errstate(invalid="ignore", divide="ignore"):
+        act = np.arange(NSNOW)[None, :] >= (np.asarray(isnow)[:, None] + NSNOW)
+        fo = r["snice"] / (r["snice"] + r["snliq"])
+    r["ficeold"] = np.where(act, fo, np.float32(0.0))
+    return r
+
+
+def soa_from_records(r):
+    """(state (56, n), isnow (n,), diag (58, n), status (n,)) of records after a call."""
+    import numpy as np
+    n = r.shape[0]
+    st = np.empty((NSTATE, n), np.float32)
+    for name, w in STATE_FIELDS:
+        o = STATE_OFF[name][0]
+        v = r[_REC_STATE.get(name, name.lower())]
+        st[o:o + w] = v.T if w > 1 else v
+    return st, r["isnow"].copy(), np.ascontiguousarray(r["out"].T), r["status"].copy()
+
+
 def _offsets(fields):
     off, out = 0, {}
     for name, w in fields:

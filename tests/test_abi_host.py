@@ -82,7 +82,7 @@ def test_params_struct_size():
 
 
 def test_abi_version_and_errors(engine_lib):
-    assert engine_lib.nmp_abi_version() == 2
+    assert engine_lib.nmp_abi_version() == 3
     for code in (0, -1, -2, -3, -4, -5, -99):
         assert engine_lib.nmp_strerror(code)
     p = _lib.NmpParams()
@@ -99,6 +99,49 @@ def test_abi_version_and_errors(engine_lib):
     zs = (C.c_float * 4)(-0.1, -0.4, -1.0, -2.0)
     assert engine_lib.nmp_step(None, 1, 1, zs, 900.0, 1.0, 366, None, None, None, None, None,
                                None, 0, None, None) == -1
+    rec = np.zeros(1, L.sflx_args_dtype())
+    assert engine_lib.nmp_sflx_columns(None, rec.ctypes.data, 1) == -1
+    assert engine_lib.nmp_sflx_column(None, rec.ctypes.data) == -1
+
+
+def test_sflx_args_layout(tmp_path):
+    """struct nmp_sflx_args (include/noahmp_engine.h) has the byte layout of
+    layout.sflx_args_dtype(): the 131 noahmp_sflx dummies in dummy order
+    (core/module_noahmp_func.f90:66-91), 4-byte members, no padding."""
+    dt = L.sflx_args_dtype()
+    names = [n for n, _, _ in L.SFLX_ARGS]
+    nargs = sum(1 for n in names if n not in ("out", "status")) + 58
+    assert nargs == 131
+    src = tmp_path / "layout.c"
+    body = "\n".join(f'printf("{n} %zu\\n", offsetof(nmp_sflx_args, {n}));' for n in names)
+    src.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "noahmp_engine.h"\n'
+                   'int main(void){printf("size %zu\\n", sizeof(nmp_sflx_args));' + body +
+                   "return 0;}\n")
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-std=c11", "-I", os.path.join(ROOT, "include"), "-o", str(exe),
+                    str(src)], check=True)
+    got = dict(line.split() for line in subprocess.run(
+        [str(exe)], capture_output=True, text=True, check=True).stdout.split("\n") if line)
+    assert int(got["size"]) == dt.itemsize
+    for n in names:
+        assert int(got[n]) == dt.fields[n][1], n
+
+
+def test_sflx_records_round_trip():
+    """SoA -> nmp_sflx_args records -> SoA is the identity (host mapping only)."""
+    from golden_io import load
+    g = load("single_casenml_mixed.npz")
+    n = 64
+    r = L.sflx_records(g["state0"][:, :n], g["isnow0"][:n], g["static_f"][:, :n],
+                       g["static_i"][:, :n], g["forcing"][:, :n], g["zsoil"], g["dt"],
+                       g["julian"], g["yearlen"])
+    st, isn, dg, status = L.soa_from_records(r)
+    assert np.array_equal(st.view(np.int32), g["state0"][:, :n].astype(np.float32).view(np.int32))
+    assert np.array_equal(isn, g["isnow0"][:n])
+    assert (r["lutyp"] == g["static_i"][0, :n]).all() and (r["isc"] == g["static_i"][3, :n]).all()
+    assert (r["cosz"] == g["forcing"][L.FORCING.index("COSZ"), :n]).all()
+    act = np.arange(3)[None, :] >= (r["isnow"][:, None] + 3)
+    assert (r["ficeold"][~act] == 0).all() and (r["ficeold"][act] > 0).all()
 
 
 def test_state_from_aos(engine_lib):

@@ -340,3 +340,50 @@ def test_ragged_and_empty(engines):
     bad, rep = column_mismatch(got, g["state1"][:, :n], 1e-5, 1e-4, STATE_NAMES)
     assert bad.sum() <= 3, rep
     assert (st.cpu().numpy()[:, n:] == 0).all(), "wrote past ncol"
+
+
+@pytest.mark.parametrize("name", ["casenml_mixed", "casenml_conus", "veg2", "fatal"])
+def test_sflx_columns_reference_calling_sequence(engines, name):
+    """nmp_sflx_columns: the 131 noahmp_sflx arguments per column (host records,
+    include/noahmp_engine.h nmp_sflx_args) give the reference's results bit for
+    bit, exactly as the SoA nmp_step path does."""
+    g = load(f"single_{name}.npz")
+    eng = engines(g["options"], tags=fixture_tags(g))
+    r = L.sflx_records(g["state0"], g["isnow0"], g["static_f"], g["static_i"], g["forcing"],
+                       g["zsoil"], g["dt"], g["julian"], g["yearlen"])
+    eng.sflx_columns(r)
+    st, isn, dg, status = L.soa_from_records(r)
+    exact = bit_equal(st, g["state1"]).all(0) & bit_equal(dg, g["diag"]).all(0) & \
+        (isn == g["isnow1"]) & (as_ref_status(status) == g["status"])
+    assert exact.all(), f"{name}: {(~exact).sum()} columns differ"
+    one = L.sflx_records(g["state0"][:, :1], g["isnow0"][:1], g["static_f"][:, :1],
+                         g["static_i"][:, :1], g["forcing"][:, :1], g["zsoil"], g["dt"],
+                         g["julian"], g["yearlen"])
+    import ctypes as C
+    assert eng._lib.nmp_sflx_column(eng._h, C.c_void_p(one.ctypes.data)) == 0
+    assert bit_equal(L.soa_from_records(one)[0], g["state1"][:, :1]).all()
+
+
+def test_sflx_columns_rejects_what_the_kernel_cannot_honour(engines):
+    """Launch-wide arguments must agree across records; FICEOLD of an active
+    layer must be the step-start ice fraction (NMP_E_ARG otherwise)."""
+    from noahmp_amd import lib as _lib
+    g = load("single_casenml_mixed.npz")
+    eng = engines(g["options"])
+    ix = np.nonzero(g["isnow0"] < 0)[0][:8]  # snow-covered columns
+    mk = lambda: L.sflx_records(g["state0"][:, ix], g["isnow0"][ix], g["static_f"][:, ix],
+                                g["static_i"][:, ix], g["forcing"][:, ix], g["zsoil"], g["dt"],
+                                g["julian"], g["yearlen"])
+    r = mk()
+    r["dt"][3] += 1.0
+    with pytest.raises(_lib.NmpError):
+        eng.sflx_columns(r)
+    r = mk()
+    r["nsoil"][0] = 5
+    with pytest.raises(_lib.NmpError):
+        eng.sflx_columns(r)
+    r = mk()
+    r["ficeold"][0, 2] = np.float32(0.123)  # layer 0 is active in every snow column
+    with pytest.raises(_lib.NmpError):
+        eng.sflx_columns(r)
+    assert eng.sflx_columns(mk()) is not None
