@@ -49,15 +49,34 @@ def bytes_per_colstep(precision: int, diag: bool) -> int:
     return b + (16 * s if diag else 0)
 
 
+def workload_name(a, n: int) -> str:
+    """BASELINE.json config this run corresponds to, else a plain description."""
+    veg = "dynamic_veg + carbon on" if a.opt_veg in (2, 5) else "dynamic_veg off"
+    if n == 1 << 20 and a.kind == "mixed" and a.precision == 4 and a.opt_veg == 1:
+        return ("config #3: 1,048,576 columns/GPU, 4 soil + 3 snow layers, dynamic_veg off, "
+                "case.nml options")
+    if n == 65536 and a.kind == "casenml" and a.precision == 8:
+        return "config #2: 65,536 replicated case.nml columns, 4 soil / 0 snow layers, fp64"
+    if a.kind == "global" and a.precision == 8 and a.opt_veg == 2:
+        return (f"config #5 per GPU: {n} columns of the 0.25-degree global grid, "
+                f"{veg}, fp64, output every {a.out_every} step(s)")
+    if a.kind == "conus":
+        return f"config #4 per GPU: {n} CONUS-like columns (all USGS/STAS types), {veg}"
+    return f"{n} {a.kind} columns/GPU, 4 soil + 3 snow layers, {veg}"
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=48)
     ap.add_argument("--warmup", type=int, default=4)
     ap.add_argument("--ncol", type=int, default=1 << 20, help="columns per GPU")
-    ap.add_argument("--kind", default="mixed", choices=("mixed", "conus", "casenml"),
+    ap.add_argument("--kind", default="mixed", choices=("mixed", "conus", "casenml", "global"),
                     help="column set: mixed (config #3), conus (config #4 types), casenml "
-                         "(replicated run/case.nml column, config #2)")
+                         "(replicated run/case.nml column, config #2), global (0.25-degree "
+                         "grid order, config #5)")
+    ap.add_argument("--opt-veg", type=int, default=1,
+                    help="dynamic vegetation option (2 = carbon model on, config #5)")
     ap.add_argument("--precision", type=int, default=4, choices=(4, 8))
     ap.add_argument("--math", default="ref", choices=("ref", "fast"))
     ap.add_argument("--dt", type=float, default=1800.0)
@@ -88,9 +107,11 @@ def main():
     from noahmp_amd.params import Params
     P = Params.builtin("STAS", "USGS")
     pdict = P.as_dict()
-    options = L.options_tuple(L.CASE_NML_OPTIONS)
+    opt_dict = dict(L.CASE_NML_OPTIONS, opt_veg=a.opt_veg)
+    options = L.options_tuple(opt_dict)
     julian0, yearlen, seed = 180.0, 366, 1000 + rank
-    cols = cases.make_columns(a.ncol, a.kind, pdict, seed=seed, julian=julian0)
+    cols = cases.make_columns(a.ncol, a.kind, pdict, seed=seed, julian=julian0,
+                              first=rank * a.ncol)
     if a.order != "as-generated":
         key = np.round(np.degrees(cols.lon) / 2.0)  # 2-degree longitude bands
         if a.order == "lon-type":
@@ -119,7 +140,7 @@ def main():
     if use_dist:
         dist.init_process_group("nccl", device_id=dev)
     dtype = torch.float32 if a.precision == 4 else torch.float64
-    eng = Engine(P, L.CASE_NML_OPTIONS, device=local, precision=a.precision, math=a.math)
+    eng = Engine(P, opt_dict, device=local, precision=a.precision, math=a.math)
     cs = ColumnState.from_host(cols, dev, dtype)
     n = cs.ncol
     F = torch.empty((a.period, L.NFORCING, n), dtype=dtype, device=dev)
@@ -218,11 +239,8 @@ def main():
             "steps": a.steps, "warmup": a.warmup, "ms_per_step": elapsed * 1e3 / a.steps,
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
             "dtype": "f32" if a.precision == 4 else "f64",
-            "data": "synthetic (seeded mixed USGS/STAS columns, diurnal forcing; no dataset)",
-            "config": {"workload": "config #3: 1,048,576 columns/GPU, 4 soil + 3 snow layers, "
-                                   "dynamic_veg off, case.nml options"
-                       if (n == 1 << 20 and a.kind == "mixed") else
-                       f"{n} {a.kind} columns/GPU, 4 soil + 3 snow layers", "kind": a.kind,
+            "data": f"synthetic (seeded {a.kind} USGS/STAS columns, diurnal forcing; no dataset)",
+            "config": {"workload": workload_name(a, n), "kind": a.kind, "opt_veg": a.opt_veg,
                        "ncol_per_gpu": n,
                        "ncol_total": world * n, "dt_s": a.dt, "out_every": a.out_every,
                        "math": a.math, "column_order": a.order,

@@ -71,7 +71,9 @@ def _month_interp(table12, julian, lat):
 
 
 def make_columns(n: int, kind: str, params: dict, seed: int = 0, julian: float = 180.0,
-                 zsoil=CASE_NML_ZSOIL) -> ColumnSet:
+                 zsoil=CASE_NML_ZSOIL, first: int = 0) -> ColumnSet:
+    """Synthetic column set.  `first`: index of the first grid cell (kind "global",
+    so the shards of a multi-GPU run tile the grid)."""
     rng = np.random.Generator(np.random.PCG64(seed))
     zsoil = np.asarray(zsoil, dtype=np.float64)
     sf = np.zeros((L.NSTATIC_F, n), np.float64)
@@ -116,6 +118,35 @@ def make_columns(n: int, kind: str, params: dict, seed: int = 0, julian: float =
         sf[L.STATIC_F.index("SHDMAX")] = np.minimum(1.0, shd + rng.uniform(0.0, 0.2, n))
         sf[L.STATIC_F.index("TBOT")] = rng.uniform(268.0, 300.0, n)
         t0 = rng.uniform(262.0, 292.0, n)     # straddles TFRZ
+        amp = rng.uniform(2.0, 9.0, n)
+        rh = rng.uniform(0.35, 0.95, n)
+        pres = rng.uniform(85000.0, 102000.0, n)
+        wind = rng.normal(0.0, 3.5, (2, n))
+        wet = rng.uniform(0.0, 0.3, n)
+    elif kind == "global":
+        # config #5: the 0.25-degree global grid (1440 x 720), row-major from the
+        # south-west corner; surface types drawn per 2-degree block (8 x 8 cells)
+        # so neighbouring columns share them, as on a real grid; climate by latitude
+        idx = (np.arange(n) + first) % (1440 * 720)
+        row, col = idx // 1440, idx % 1440
+        lat = np.radians(-89.875 + 0.25 * (row % 720))
+        lon = np.radians(-179.875 + 0.25 * col)
+        blk = (row // 8) * 180 + col // 8
+        nblk = int(blk.max()) + 1
+        blut = rng.integers(1, params["nlutyp"] + 1, nblk)
+        land_soils = np.array([s for s in range(1, params["nsltyp"] + 1) if s != 14])
+        bslt = rng.choice(land_soils, nblk)
+        lut = blut[blk]
+        alat = np.abs(np.degrees(lat))
+        lut = np.where(alat > 66.0, np.where((blk % 3) == 0, isice, lut), lut)
+        slt = np.where(lut == iswater, 14, np.where(lut == isice, 16, bslt[blk]))
+        isc = rng.integers(1, 9, nblk)[blk]
+        slope = rng.integers(1, 10, nblk)[blk]
+        shd = rng.uniform(0.05, 0.95, nblk)[blk]
+        sf[L.STATIC_F.index("SHDFAC")] = shd
+        sf[L.STATIC_F.index("SHDMAX")] = np.minimum(1.0, shd + rng.uniform(0.0, 0.2, n))
+        t0 = 301.0 - 45.0 * np.abs(np.sin(lat)) ** 1.5 + rng.normal(0.0, 1.5, n)
+        sf[L.STATIC_F.index("TBOT")] = t0 - 3.0 + rng.uniform(-1.0, 1.0, n)
         amp = rng.uniform(2.0, 9.0, n)
         rh = rng.uniform(0.35, 0.95, n)
         pres = rng.uniform(85000.0, 102000.0, n)

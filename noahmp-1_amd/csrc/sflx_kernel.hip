@@ -2717,18 +2717,23 @@ DEV void sflx_column(const DevParams& P, const KArgs<T>& A, Col<T>& c, const Sin
 
 // ---------------------------------------------------------------------------
 template <class T, bool R>
-// Occupancy target: 4 waves/SIMD for fp32 (128 VGPRs), 1 for fp64.  With the
-// launch tails overlapped by two stream ranges (engine.StreamShards) 4 waves
+// Occupancy target: 4 waves/SIMD for fp32 (128 VGPRs), 2 for fp64 (256).  With
+// the launch tails overlapped by two stream ranges (engine.StreamShards) 4 waves
 // measured 1,175 Mcs/s against 1,131 at 3 (168 VGPRs, fewer spills), 921 at 2
-// and 930 at 5 (tools/sweep.sh; DESIGN.md "Occupancy").
+// and 930 at 5 (tools/sweep.sh; DESIGN.md "Occupancy").  fp64 on config #5
+// (global grid, carbon on): 645 Mcs/s at 2 waves, 534 at 3, 453 at 1 (no
+// spills, 378 VGPRs) (tools/configs.sh).
 #ifndef NMP_WAVES_PER_EU
 #define NMP_WAVES_PER_EU 4
+#endif
+#ifndef NMP_WAVES_PER_EU_F64
+#define NMP_WAVES_PER_EU_F64 2
 #endif
 #ifndef NMP_BLOCK
 #define NMP_BLOCK 256
 #endif
 __global__ __launch_bounds__(NMP_BLOCK)
-__attribute__((amdgpu_waves_per_eu(sizeof(T) == 4 ? NMP_WAVES_PER_EU : 1)))
+__attribute__((amdgpu_waves_per_eu(sizeof(T) == 4 ? NMP_WAVES_PER_EU : NMP_WAVES_PER_EU_F64)))
 void sflx_step_kernel(const DevParams* __restrict__ gparams,
                                                           KArgs<T> a) {
   __shared__ __attribute__((aligned(16))) DevParams sp;

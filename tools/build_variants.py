@@ -29,6 +29,8 @@ VARIANTS = {
     "w4_b128": ("-DNMP_WAVES_PER_EU=4", "-DNMP_BLOCK=128"),
     "w4_b64": ("-DNMP_WAVES_PER_EU=4", "-DNMP_BLOCK=64"),
     "w5": ("-DNMP_WAVES_PER_EU=5",),
+    "d2": ("-DNMP_WAVES_PER_EU_F64=2",),
+    "d3": ("-DNMP_WAVES_PER_EU_F64=3",),
     "mlicm": ("-mllvm", "-disable-machine-licm=false"),
     "w4_mlicm": ("-DNMP_WAVES_PER_EU=4", "-mllvm", "-disable-machine-licm=false"),
 }
