@@ -1900,6 +1900,9 @@ DEV void sflx_column(const DevParams& P, const KArgs<T>& A, Col<T>& c, const Sin
   const T edir = qvap - qdew;
   out.template d<NMP_D_EDIR>(edir);
   out.s(NMP_S_SNEQVO, c.sneqvo);
+#ifdef NMP_TRUNC_ENERGY
+  return;  // timing experiment only (tools/build_variants.py): the energy phase alone
+#endif
 
   NMP_PHASE(9);
   // ===================== water: func.f90:4601-4804 =====================

@@ -29,7 +29,17 @@ VARIANTS = {
     "w4_b128": ("-DNMP_WAVES_PER_EU=4", "-DNMP_BLOCK=128"),
     "w4_b64": ("-DNMP_WAVES_PER_EU=4", "-DNMP_BLOCK=64"),
     "w5": ("-DNMP_WAVES_PER_EU=5",),
+    "d1": ("-DNMP_WAVES_PER_EU_F64=1",),
+    "en_w4": ("-DNMP_TRUNC_ENERGY",),
+    "en_w5": ("-DNMP_TRUNC_ENERGY", "-DNMP_WAVES_PER_EU=5"),
+    "en_w3": ("-DNMP_TRUNC_ENERGY", "-DNMP_WAVES_PER_EU=3"),
     "d2": ("-DNMP_WAVES_PER_EU_F64=2",),
+    "s_maxilp": ("-mllvm", "-amdgpu-sched-strategy=max-ilp"),
+    "s_memclause": ("-mllvm", "-amdgpu-sched-strategy=max-memory-clause"),
+    "s_itminreg": ("-mllvm", "-amdgpu-sched-strategy=iterative-minreg"),
+    "s_itilp": ("-mllvm", "-amdgpu-sched-strategy=iterative-ilp"),
+    "s_nomisched": ("-mllvm", "-enable-misched=false"),
+    "s_postup": ("-mllvm", "-misched-postra-direction=bottomup"),
     "d3": ("-DNMP_WAVES_PER_EU_F64=3",),
     "mlicm": ("-mllvm", "-disable-machine-licm=false"),
     "w4_mlicm": ("-DNMP_WAVES_PER_EU=4", "-mllvm", "-disable-machine-licm=false"),
