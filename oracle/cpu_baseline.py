@@ -30,8 +30,19 @@ def default_workers(cap: int = 16) -> int:
     return max(1, min(n, cap))
 
 
+def cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def _worker(args):
-    i, kind, cols_per, nsteps, t_start = args
+    i, kind, cols_per, nsteps, t_start, precision = args
     from noahmp_amd import cases  # package registered by the parent
     c = _CTX
     cols = c["cols"].take(np.arange(i * cols_per, (i + 1) * cols_per))
@@ -55,7 +66,7 @@ def _worker(args):
         time.sleep(0.001)
     t0 = time.perf_counter()
     port.run(c["params"], c["options"], c["zsoil"], c["dt"], c["yearlen"], c["julian0"], st, isn,
-             cols.static_f, cols.static_i, Fa, nsteps)
+             cols.static_f, cols.static_i, Fa, nsteps, precision=precision)
     return time.perf_counter() - t0
 
 
@@ -72,13 +83,25 @@ def measure(cols, params: dict, options: tuple, zsoil, dt: float, julian0: float
     cols_per_worker = min(cols_per_worker, cols.n // workers)
     _CTX.update(cols=cols, params=params, options=options, zsoil=np.asarray(zsoil, np.float32),
                 dt=dt, julian0=julian0, yearlen=yearlen, seed=seed, period=period)
-    t_start = time.time() + 2.0 + 0.02 * workers
-    with mp.get_context("fork").Pool(workers) as pool:
-        el = pool.map(_worker, [(i, kind, cols_per_worker, nsteps, t_start) for i in range(workers)])
-    wall = max(el)
+    def timed(kind, precision):
+        t_start = time.time() + 2.0 + 0.02 * workers
+        with mp.get_context("fork").Pool(workers) as pool:
+            el = pool.map(_worker, [(i, kind, cols_per_worker, nsteps, t_start, precision)
+                                    for i in range(workers)])
+        return max(el)
+
+    wall = timed(kind, 4)
     total = workers * cols_per_worker * nsteps
-    return {"value": total / wall, "unit": "column-steps/s", "cores": workers, "kind": kind,
-            "sample": (f"{workers} single-threaded processes x {cols_per_worker} columns x "
-                       f"{nsteps} steps of the bench column set "
-                       f"({'Fortran reference noahmp_sflx, amdflang -O2' if kind == 'reference' else 'C restatement -O2'}"
-                       f"), wall {wall:.1f} s")}
+    out = {"value": total / wall, "unit": "column-steps/s", "cores": workers, "kind": kind,
+           "sample": (f"{workers} single-threaded processes x {cols_per_worker} columns x "
+                      f"{nsteps} steps of the bench column set "
+                      f"({'Fortran reference noahmp_sflx, amdflang -O2' if kind == 'reference' else 'C restatement -O2'}"
+                      f"), wall {wall:.1f} s"),
+           "cpu_model": cpu_model(), "affinity_cores": len(os.sched_getaffinity(0))}
+    if port.available(8):
+        # fp64 leg (SURVEY 8d asks for both precisions): the C restatement in
+        # double, same processes / sample (the reference itself is fp32-only, H11)
+        w8 = timed("port", 8)
+        out["port_f64"] = {"value": total / w8, "unit": "column-steps/s", "cores": workers,
+                           "sample": f"C restatement fp64 -O2, same sample, wall {w8:.1f} s"}
+    return out
