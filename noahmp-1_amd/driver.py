@@ -11,10 +11,15 @@ offline/noahmp_config.py has no time loop, forcing reader or writer, SURVEY
   reference's LDASIN files are not in the repository, so `SyntheticForcing`
   (the seeded diurnal generator the tests and bench use) is the default;
 * output steps (Config.output_frequency) write the 16 surface fluxes as
-  ``<outdir>/<YYYYMMDDHH>.LDASOUT.npz``;
+  ``<outdir>/<YYYYMMDDHH>.LDASOUT_DOMAIN1`` (netCDF-3 on the grid, ncio.py)
+  when the columns come from a grid, else ``<outdir>/<YYYYMMDDHH>.LDASOUT.npz``;
 * restart steps (Config.restart_frequency, calendar months allowed) write the
-  complete SoA state as ``<resdir>/RESTART.<YYYYMMDDHH>.npz``, which
-  `load_restart` reads back -- the state SoA *is* the restart.
+  complete SoA state (``RESTART.<YYYYMMDDHH>_DOMAIN1.nc`` on a grid, else
+  ``.npz``), which `load_restart` reads back -- the state SoA *is* the restart
+  (SURVEY 8f item 2);
+* `OfflineDriver.from_files` builds the run from the namelist's files: the
+  static file (grid, types), the initialization file (state) and the LDASIN
+  directory (forcing), all netCDF-3 (ncio.py).
 
 Multi-rank: each rank drives its own column shard; at output steps the
 diagnostics are all-gathered (shard.gather_diag) and rank 0 writes them.
@@ -28,7 +33,7 @@ import numpy as np
 import torch
 import torch.distributed as dist
 
-from . import cases, layout as L, shard, timeman
+from . import cases, layout as L, ncio, shard, timeman
 from .config import Config
 from .engine import ColumnState, Engine, StreamShards
 from .params import Params
@@ -64,8 +69,9 @@ class OfflineDriver:
     def __init__(self, cfg: Config, cols: cases.ColumnSet, device: int = 0,
                  params: Params | None = None, forcing=None, precision: int = 4,
                  math: str = "ref", zsoil=cases.CASE_NML_ZSOIL, write: bool = True,
-                 streams: int = 2):
+                 streams: int = 2, grid: ncio.Grid | None = None):
         self.cfg = cfg
+        self.grid = grid
         self.engine = Engine(params or Params.builtin(), cfg.engine_options(), device, precision,
                              math)
         self.dtype = self.engine.dtype
@@ -82,9 +88,28 @@ class OfflineDriver:
         self.diag = torch.zeros((L.NDIAG_OUT, self.cs.ncol), dtype=self.dtype, device=self.dev)
         self.written = []
 
+    @classmethod
+    def from_files(cls, cfg: Config, device: int = 0, params: Params | None = None,
+                   init: str | None = None, **kw) -> "OfflineDriver":
+        """The run the namelist describes: static file (cfg.constfile), initial
+        state (cfg.initfile, or `init`) and LDASIN forcing (cfg.indir every
+        cfg.input_frequency), netCDF-3 files in the layouts of ncio.py."""
+        P = params or Params.builtin()
+        grid, sf, si = ncio.read_static(cfg.constfile, P.as_dict(), cfg.begdatetime)
+        st, isn, t0, step = ncio.read_state(init or cfg.initfile, grid)
+        cols = cases.ColumnSet(sf, si, st, isn, grid.lon_rad, *([None] * 6))
+        forcing = ncio.LdasinForcing(cfg.indir, grid, cfg.begdatetime, cfg.input_interval)
+        drv = cls(cfg, cols, device, P, forcing, grid=grid, **kw)
+        drv.t, drv.step_index = t0, step
+        return drv
+
     # ---- restart -----------------------------------------------------------------
     def save_restart(self, path: str):
         self.ranges.join()
+        if path.endswith(".nc"):
+            ncio.write_state(path, self.grid, self.cs.state.cpu().numpy(),
+                             self.cs.isnow.cpu().numpy(), self.t, self.step_index)
+            return
         np.savez(path, time=np.array(self.t.isoformat()), step=np.int64(self.step_index),
                  state=self.cs.state.cpu().numpy(), isnow=self.cs.isnow.cpu().numpy(),
                  static_f=self.cs.static_f.cpu().numpy(), static_i=self.cs.static_i.cpu().numpy(),
@@ -93,6 +118,12 @@ class OfflineDriver:
 
     def load_restart(self, path: str):
         self.ranges.join()  # no range may still be stepping the state being replaced
+        if path.endswith(".nc"):
+            st, isn, self.t, self.step_index = ncio.read_state(path, self.grid,
+                                                               self.cs.state.cpu().numpy().dtype)
+            self.cs.state.copy_(torch.as_tensor(st, device=self.dev))
+            self.cs.isnow.copy_(torch.as_tensor(isn, device=self.dev))
+            return
         with np.load(path, allow_pickle=False) as z:
             assert str(z["layout"]) == ",".join(n for n, _ in L.STATE_FIELDS), "state layout"
             for name in ("state", "isnow", "static_f", "static_i", "status"):
@@ -124,13 +155,19 @@ class OfflineDriver:
                 d = shard.gather_diag(self.diag) if dist.is_initialized() else self.diag
                 if rank == 0:
                     os.makedirs(cfg.outdir, exist_ok=True)
-                    path = os.path.join(cfg.outdir, f"{_stamp(t1)}.LDASOUT.npz")
-                    np.savez(path, time=np.array(t1.isoformat()),
-                             fields=np.array(",".join(L.DIAG_OUT)), diag=d.cpu().numpy())
+                    if self.grid is not None:
+                        path = ncio.ldasout_path(cfg.outdir, t1)
+                        ncio.write_ldasout(path, self.grid, d.cpu().numpy(), t1)
+                    else:
+                        path = os.path.join(cfg.outdir, f"{_stamp(t1)}.LDASOUT.npz")
+                        np.savez(path, time=np.array(t1.isoformat()),
+                                 fields=np.array(",".join(L.DIAG_OUT)), diag=d.cpu().numpy())
                     self.written.append(path)
             if _is_boundary(t1, cfg.begdatetime, res_every) and self.write:
                 os.makedirs(cfg.resdir, exist_ok=True)
-                self.save_restart(os.path.join(cfg.resdir, f"RESTART.{_stamp(t1)}.r{rank}.npz"))
+                name = (f"RESTART.{_stamp(t1)}_DOMAIN1.nc" if self.grid is not None and
+                        not dist.is_initialized() else f"RESTART.{_stamp(t1)}.r{rank}.npz")
+                self.save_restart(os.path.join(cfg.resdir, name))
         self.ranges.join()
         torch.cuda.synchronize(self.dev)
         return self

@@ -1,0 +1,329 @@
+"""netCDF-3 files of the offline run: static grid, initial/restart state,
+LDASIN forcing and LDASOUT output.
+
+The reference names these files in its namelist (run/case.nml:2-11:
+static_parameter_file, initialization_file, restart_file, input_directory,
+output_directory) but ships no reader or writer for them (run/main.py stops
+after the namelist).  This module supplies them in the
+HRLDAS conventions Noah-MP offline runs use, as netCDF-3 classic files through
+scipy.io.netcdf_file (no netCDF-4/HDF5 library exists in this image):
+
+* static file (geo_em-style), dims (south_north, west_east[, month]):
+  XLAT_M, XLONG_M (deg), LANDMASK, LU_INDEX (vegetation type), SCT_DOM (soil
+  type), SLOPECAT, SOILCOLOR, SOILTEMP (deep soil T -> TBOT), GREENFRAC
+  (12 monthly fractions -> SHDFAC by the date), SHDMAX (default: the
+  GREENFRAC maximum), ZLVL, FOLN,
+  ISLAKE/ISICE from the table's ISWATER/ISICE types;
+* LDASIN, one file per input time, ``<YYYYMMDDHH>.LDASIN_DOMAIN1``:
+  T2D, Q2D, U2D, V2D, PSFC, RAINRATE, SWDOWN, LWDOWN on (Time, south_north,
+  west_east).  Optional extras COSZ, CO2AIR, O2AIR override the derived values
+  (COSZ from the grid's lat/lon at the step's time, CO2AIR = 395e-6 PSFC,
+  O2AIR = 0.209 PSFC);
+* state file (initialization_file / restart_file): the engine's SoA state,
+  one variable per state field (layer fields get a layer dimension), ISNOW,
+  plus the model time -- the state SoA *is* the restart;
+* LDASOUT, one file per output time, ``<YYYYMMDDHH>.LDASOUT_DOMAIN1``: the 16
+  output fluxes on the grid, _FillValue off the land mask.
+
+Columns are the grid's land points (LANDMASK == 1) in row-major order.
+"""
+from __future__ import annotations
+
+import datetime
+import os
+
+import numpy as np
+from scipy.io import netcdf_file
+
+from . import cases, layout as L, timeman
+
+FILL = np.float32(-9999.0)
+LDASIN_MAP = {"SFCTMP": "T2D", "Q2": "Q2D", "UU": "U2D", "VV": "V2D", "SFCPRS": "PSFC",
+              "PSFC": "PSFC", "PRCP": "RAINRATE", "SOLDN": "SWDOWN", "LWDN": "LWDOWN"}
+LDASIN_UNITS = {"T2D": "K", "Q2D": "kg kg-1", "U2D": "m s-1", "V2D": "m s-1", "PSFC": "Pa",
+                "RAINRATE": "kg m-2 s-1", "SWDOWN": "W m-2", "LWDOWN": "W m-2",
+                "COSZ": "1", "CO2AIR": "Pa", "O2AIR": "Pa"}
+_LAYER_DIMS = {7: "snso_layers", 4: "soil_layers", 3: "snow_layers"}
+
+
+def stamp(t: datetime.datetime) -> str:
+    """HRLDAS file-time stamp YYYYMMDDHH; minutes are appended for off-hour
+    times (input or output intervals below an hour)."""
+    return t.strftime("%Y%m%d%H" if t.minute == 0 and t.second == 0 else "%Y%m%d%H%M")
+
+
+def ldasin_path(indir: str, t: datetime.datetime) -> str:
+    return os.path.join(indir, f"{stamp(t)}.LDASIN_DOMAIN1")
+
+
+def ldasout_path(outdir: str, t: datetime.datetime) -> str:
+    return os.path.join(outdir, f"{stamp(t)}.LDASOUT_DOMAIN1")
+
+
+def _read(path: str):
+    if not os.path.isfile(path):
+        raise FileNotFoundError(path)
+    return netcdf_file(path, "r", mmap=False)
+
+
+# ---- grid -------------------------------------------------------------------------
+class Grid:
+    """Land points of a (south_north, west_east) grid, row-major."""
+
+    def __init__(self, lat_deg: np.ndarray, lon_deg: np.ndarray, mask: np.ndarray):
+        self.shape = tuple(mask.shape)
+        self.lat_deg = np.asarray(lat_deg, np.float64)
+        self.lon_deg = np.asarray(lon_deg, np.float64)
+        self.mask = np.asarray(mask, bool)
+        self.index = np.flatnonzero(self.mask.reshape(-1))
+
+    @property
+    def n(self) -> int:
+        return int(self.index.size)
+
+    def columns(self, field2d: np.ndarray) -> np.ndarray:
+        return np.asarray(field2d).reshape(-1)[self.index]
+
+    def scatter(self, cols: np.ndarray, fill=FILL) -> np.ndarray:
+        out = np.full(self.shape[0] * self.shape[1], fill, np.asarray(cols).dtype)
+        out[self.index] = cols
+        return out.reshape(self.shape)
+
+    @property
+    def lat_rad(self) -> np.ndarray:
+        return np.radians(self.columns(self.lat_deg))
+
+    @property
+    def lon_rad(self) -> np.ndarray:
+        return np.radians(self.columns(self.lon_deg))
+
+
+# ---- static file ----------------------------------------------------------------
+def write_static(path: str, cols: cases.ColumnSet, grid: Grid, greenfrac=None):
+    """A geo_em-style static file for `cols` laid on `grid` (tests / examples)."""
+    ny, nx = grid.shape
+    f = netcdf_file(path, "w")
+    try:
+        f.createDimension("south_north", ny)
+        f.createDimension("west_east", nx)
+        f.createDimension("month", 12)
+        dims = ("south_north", "west_east")
+
+        def put(name, data, kind="f4", units=None):
+            v = f.createVariable(name, kind, dims)
+            v[:] = data
+            if units:
+                v.units = units
+
+        # f8 degrees: radians -> degrees -> radians returns the columns' f32 LAT exactly
+        put("XLAT_M", grid.lat_deg, "f8", units="degrees_north")
+        put("XLONG_M", grid.lon_deg, "f8", units="degrees_east")
+        put("LANDMASK", grid.mask.astype(np.int32), "i4")
+        sf, si = cols.static_f, cols.static_i
+        for name, row in (("LU_INDEX", "VEGTYP"), ("SCT_DOM", "SOILTYP"), ("SLOPECAT", "SLOPETYP"),
+                          ("SOILCOLOR", "SOILCOLOR")):
+            put(name, grid.scatter(si[L.STATIC_I.index(row)].astype(np.int32), 0), "i4")
+        put("SOILTEMP", grid.scatter(sf[L.STATIC_F.index("TBOT")]), units="K")
+        put("ZLVL", grid.scatter(sf[L.STATIC_F.index("ZLVL")]), units="m")
+        put("FOLN", grid.scatter(sf[L.STATIC_F.index("FOLN")]))
+        if greenfrac is None:  # constant in time: the columns' SHDFAC every month
+            greenfrac = np.repeat(sf[L.STATIC_F.index("SHDFAC")][None, :], 12, 0)
+        put("SHDMAX", grid.scatter(sf[L.STATIC_F.index("SHDMAX")]))
+        v = f.createVariable("GREENFRAC", "f4", ("month",) + dims)
+        v[:] = np.stack([grid.scatter(np.asarray(g, np.float32)) for g in greenfrac])
+    finally:
+        f.close()
+
+
+def read_static(path: str, params: dict, when: datetime.datetime):
+    """(Grid, static_f (6, n) f32, static_i (6, n) i32) of a static file.
+    SHDFAC is GREENFRAC interpolated to `when` (mid-month weights), SHDMAX its
+    annual maximum; IST = 2 on the table's water type, ICE = 1 on its ice type."""
+    f = _read(path)
+    try:
+        v = f.variables
+        lat, lon = np.array(v["XLAT_M"][:]), np.array(v["XLONG_M"][:])
+        mask = np.array(v["LANDMASK"][:]) == 1 if "LANDMASK" in v else np.ones(lat.shape, bool)
+        grid = Grid(lat, lon, mask)
+        n = grid.n
+        col = lambda name, default: (grid.columns(np.array(v[name][:])) if name in v  # noqa: E731
+                                     else np.full(n, default))
+        lut = col("LU_INDEX", 7).astype(np.int32)
+        slt = col("SCT_DOM", 6).astype(np.int32)
+        gf = np.array(v["GREENFRAC"][:]) if "GREENFRAC" in v else None
+        sf = np.zeros((L.NSTATIC_F, n), np.float32)
+        si = np.zeros((L.NSTATIC_I, n), np.int32)
+        sf[L.STATIC_F.index("LAT")] = np.radians(grid.columns(lat))
+        sf[L.STATIC_F.index("ZLVL")] = col("ZLVL", 10.0)
+        sf[L.STATIC_F.index("TBOT")] = col("SOILTEMP", 285.0)
+        sf[L.STATIC_F.index("FOLN")] = col("FOLN", 1.0)
+        if gf is not None:
+            g = np.stack([grid.columns(gf[m]) for m in range(12)])
+            sf[L.STATIC_F.index("SHDFAC")] = _month_weighted(g, when)
+            sf[L.STATIC_F.index("SHDMAX")] = col("SHDMAX", 0.0) if "SHDMAX" in v else g.max(0)
+        else:
+            sf[L.STATIC_F.index("SHDFAC")] = 0.7
+            sf[L.STATIC_F.index("SHDMAX")] = 0.8
+        si[L.STATIC_I.index("VEGTYP")] = lut
+        si[L.STATIC_I.index("SOILTYP")] = slt
+        si[L.STATIC_I.index("SLOPETYP")] = col("SLOPECAT", 1)
+        si[L.STATIC_I.index("SOILCOLOR")] = col("SOILCOLOR", 4)
+        si[L.STATIC_I.index("IST")] = np.where(lut == params["iswater"], 2, 1)
+        si[L.STATIC_I.index("ICE")] = np.where(lut == params["isice"], 1, 0)
+        return grid, sf, si
+    finally:
+        f.close()
+
+
+def _month_weighted(g12: np.ndarray, when: datetime.datetime) -> np.ndarray:
+    """Linear interpolation between mid-month values (a monthly climatology at `when`)."""
+    ylen = timeman.yearlen(when.year)
+    t = 12.0 * timeman.julian(when) / ylen - 0.5
+    m0 = int(np.floor(t)) % 12
+    w = t - np.floor(t)
+    return ((1.0 - w) * g12[m0] + w * g12[(m0 + 1) % 12]).astype(np.float32)
+
+
+# ---- state (initialization / restart) ----------------------------------------------
+def write_state(path: str, grid: Grid, state: np.ndarray, isnow: np.ndarray,
+                t: datetime.datetime, step: int = 0):
+    """SoA state (56, n) + ISNOW on the grid; layer fields get a layer dimension."""
+    ny, nx = grid.shape
+    f = netcdf_file(path, "w")
+    try:
+        f.createDimension("south_north", ny)
+        f.createDimension("west_east", nx)
+        for w, d in _LAYER_DIMS.items():
+            f.createDimension(d, w)
+        f.model_time = t.isoformat()
+        f.model_step = np.int32(step)
+        f.state_layout = ",".join(n for n, _ in L.STATE_FIELDS)
+        dims = ("south_north", "west_east")
+        kind = "f8" if state.dtype == np.float64 else "f4"
+        for name, w in L.STATE_FIELDS:
+            o = L.STATE_OFF[name][0]
+            if w == 1:
+                v = f.createVariable(name, kind, dims)
+                v[:] = grid.scatter(state[o].astype(kind), np.asarray(FILL, kind))
+            else:
+                v = f.createVariable(name, kind, (_LAYER_DIMS[w],) + dims)
+                v[:] = np.stack([grid.scatter(state[o + k].astype(kind), np.asarray(FILL, kind))
+                                 for k in range(w)])
+        v = f.createVariable("ISNOW", "i4", dims)
+        v[:] = grid.scatter(isnow.astype(np.int32), 0)
+    finally:
+        f.close()
+
+
+def read_state(path: str, grid: Grid, dtype=np.float32):
+    """(state (56, n), isnow (n,), time, step) from a state file on `grid`."""
+    f = _read(path)
+    try:
+        layout = f.state_layout.decode() if isinstance(f.state_layout, bytes) else f.state_layout
+        assert layout == ",".join(n for n, _ in L.STATE_FIELDS), "state layout"
+        st = np.zeros((L.NSTATE, grid.n), dtype)
+        for name, w in L.STATE_FIELDS:
+            o = L.STATE_OFF[name][0]
+            a = np.array(f.variables[name][:])
+            if w == 1:
+                st[o] = grid.columns(a)
+            else:
+                for k in range(w):
+                    st[o + k] = grid.columns(a[k])
+        isnow = grid.columns(np.array(f.variables["ISNOW"][:])).astype(np.int32)
+        mt = f.model_time.decode() if isinstance(f.model_time, bytes) else f.model_time
+        return st, isnow, datetime.datetime.fromisoformat(mt), int(f.model_step)
+    finally:
+        f.close()
+
+
+# ---- LDASIN ---------------------------------------------------------------------
+def write_ldasin(path: str, grid: Grid, forcing: np.ndarray, t: datetime.datetime,
+                 extras: bool = True):
+    """One LDASIN file from a (12, n) forcing slice; `extras` also stores COSZ,
+    CO2AIR and O2AIR so the file reproduces the slice exactly."""
+    ny, nx = grid.shape
+    f = netcdf_file(path, "w")
+    try:
+        f.createDimension("Time", None)
+        f.createDimension("south_north", ny)
+        f.createDimension("west_east", nx)
+        f.valid_time = t.isoformat()
+        dims = ("Time", "south_north", "west_east")
+        names = dict(LDASIN_MAP)
+        names.pop("SFCPRS")  # SFCPRS and PSFC share the PSFC variable
+        if extras:
+            names.update(COSZ="COSZ", CO2AIR="CO2AIR", O2AIR="O2AIR")
+        for fld, var in names.items():
+            v = f.createVariable(var, "f4", dims)
+            v[0] = grid.scatter(forcing[L.FORCING.index(fld)].astype(np.float32))
+            v.units = LDASIN_UNITS[var]
+    finally:
+        f.close()
+
+
+def read_ldasin(path: str) -> dict:
+    f = _read(path)
+    try:
+        return {k: np.array(v[0] if v.dimensions[0] == "Time" else v[:])
+                for k, v in f.variables.items()}
+    finally:
+        f.close()
+
+
+class LdasinForcing:
+    """Forcing provider for driver.OfflineDriver from LDASIN files: the file of
+    the latest input time <= the step's start time (input_frequency, counted
+    from the run's start), held constant over the input interval."""
+
+    def __init__(self, indir: str, grid: Grid, begin: datetime.datetime,
+                 every: datetime.timedelta):
+        self.indir, self.grid, self.begin, self.every = indir, grid, begin, every
+        self._t, self._fields = None, None
+
+    def input_time(self, t: datetime.datetime) -> datetime.datetime:
+        k = (t - self.begin) // self.every
+        return self.begin + k * self.every
+
+    def __call__(self, step: int, t: datetime.datetime) -> np.ndarray:
+        ti = self.input_time(t)
+        if ti != self._t:
+            raw = read_ldasin(ldasin_path(self.indir, ti))
+            self._fields = {k: self.grid.columns(v) for k, v in raw.items()}
+            self._t = ti
+        fl = self._fields
+        n = self.grid.n
+        f = np.empty((L.NFORCING, n), np.float32)
+        for fld, var in LDASIN_MAP.items():
+            f[L.FORCING.index(fld)] = fl[var]
+        psfc = fl["PSFC"].astype(np.float64)
+        f[L.FORCING.index("COSZ")] = fl["COSZ"] if "COSZ" in fl else timeman.cosz(
+            self.grid.lat_rad, self.grid.lon_rad, timeman.julian(t), timeman.yearlen(t.year))
+        f[L.FORCING.index("CO2AIR")] = fl["CO2AIR"] if "CO2AIR" in fl else 395.0e-6 * psfc
+        f[L.FORCING.index("O2AIR")] = fl["O2AIR"] if "O2AIR" in fl else 0.209 * psfc
+        return f
+
+
+# ---- LDASOUT ----------------------------------------------------------------------
+def write_ldasout(path: str, grid: Grid, diag: np.ndarray, t: datetime.datetime):
+    """The 16 output fluxes (NMP_O_*, (16, n)) on the grid."""
+    ny, nx = grid.shape
+    f = netcdf_file(path, "w")
+    try:
+        f.createDimension("Time", None)
+        f.createDimension("south_north", ny)
+        f.createDimension("west_east", nx)
+        f.valid_time = t.isoformat()
+        dims = ("Time", "south_north", "west_east")
+        kind = "f8" if diag.dtype == np.float64 else "f4"
+        for i, name in enumerate(L.DIAG_OUT):
+            v = f.createVariable(name, kind, dims)
+            v._FillValue = np.asarray(FILL, kind)
+            v[0] = grid.scatter(diag[i].astype(kind), np.asarray(FILL, kind))
+    finally:
+        f.close()
+
+
+def read_ldasout(path: str, grid: Grid) -> np.ndarray:
+    raw = read_ldasin(path)
+    return np.stack([grid.columns(raw[name]) for name in L.DIAG_OUT])

@@ -6,10 +6,16 @@
 
 Reads the namelist like the reference (noahmp_amd.config.Config ==
 offline/noahmp_config.Config) and then does what the reference driver does
-not yet do: runs the time loop through the engine (noahmp_amd.driver).  The
-reference's static/init/LDASIN files are not part of the repository, so the
-columns and forcing are the seeded synthetic set (`--kind casenml` = the
-run/case.nml column of SURVEY 8d config #1, replicated --ncol times).
+not yet do: runs the time loop through the engine (noahmp_amd.driver).
+
+When the namelist's static_parameter_file exists, the run comes from files
+(netCDF-3, noahmp_amd/ncio.py): grid and surface types from the static file,
+the state from initialization_file (or --restart), forcing from the LDASIN
+files in input_directory; output goes to LDASOUT files.
+`tools/make_offline_case.py` writes such a set from the synthetic generator.
+Otherwise the columns and forcing are the seeded synthetic set (`--kind
+casenml` = the run/case.nml column of SURVEY 8d config #1, replicated --ncol
+times).
 """
 import argparse
 import os
@@ -30,17 +36,21 @@ def main(argv=None):
     ap = argparse.ArgumentParser(description="Noah-MP Land Surface Model (MI355X engine)")
     ap.add_argument("nmlfile", nargs="?", default=DEFAULT_NAMELIST_FILE, help="configuration file")
     ap.add_argument("--ncol", type=int, default=1)
-    ap.add_argument("--kind", default="casenml", choices=("casenml", "mixed", "conus"))
+    ap.add_argument("--kind", default="casenml", choices=("casenml", "mixed", "conus", "global"))
     ap.add_argument("--device", type=int, default=0)
     ap.add_argument("--restart", default=None, help="restart file to start from")
     a = ap.parse_args(argv)
     cfg = config.Config(a.nmlfile)
     P = Params.builtin()
-    cols = cases.make_columns(a.ncol, a.kind, P.as_dict(), seed=0,
-                              julian=timeman.julian(cfg.begdatetime))
-    drv = driver.OfflineDriver(cfg, cols, device=a.device, params=P)
-    if a.restart:
-        drv.load_restart(a.restart)
+    if os.path.isfile(cfg.constfile):
+        drv = driver.OfflineDriver.from_files(cfg, device=a.device, params=P, init=a.restart)
+        a.ncol = drv.cs.ncol
+    else:
+        cols = cases.make_columns(a.ncol, a.kind, P.as_dict(), seed=0,
+                                  julian=timeman.julian(cfg.begdatetime))
+        drv = driver.OfflineDriver(cfg, cols, device=a.device, params=P)
+        if a.restart:
+            drv.load_restart(a.restart)
     t0 = time.perf_counter()
     drv.run()
     el = time.perf_counter() - t0

@@ -56,3 +56,73 @@ def test_restart_round_trip(engine_lib, tmp_path):
     assert b.step_index == 40
     b.run()
     assert bit_equal(b.cs.state.cpu().numpy(), g["states"][-1]).all()
+
+
+def test_driver_from_netcdf_files(engine_lib, tmp_path):
+    """namelist -> static / init / LDASIN netCDF files (ncio.py) -> time loop ->
+    LDASOUT netCDF and a netCDF restart: the reference trajectory bit for bit."""
+    from noahmp_amd import ncio
+    from test_config import write_case
+    from test_ncio import grid_for
+    g = load("traj_casenml.npz")
+    cols = _cols(g)
+    grid = grid_for(cols)
+    static, init, indir = tmp_path / "geo_em.d01.nc", tmp_path / "init.nc", tmp_path / "ldasin"
+    indir.mkdir()
+    nml = write_case(tmp_path)
+    text = open(nml).read().replace("'geo_em.d01.nc'", f"'{static}'").replace(
+        '"init.nc"', f'"{init}"').replace("'ldasin'", f"'{indir}'").replace(
+        "'1 hour'", "'900 second'")
+    open(nml, "w").write(text)
+    cfg = config.Config(nml)
+    ncio.write_static(str(static), cols, grid)
+    ncio.write_state(str(init), grid, g["state0"], g["isnow0"], cfg.begdatetime)
+    for k, t in enumerate([cfg.begdatetime + i * cfg.timestep for i in range(96)]):
+        ncio.write_ldasin(ncio.ldasin_path(str(indir), t), grid, g["forcing"][k], t)
+    drv = driver.OfflineDriver.from_files(cfg)
+    drv.run()
+    assert drv.step_index == 96
+    assert bit_equal(drv.cs.state.cpu().numpy(), g["states"][-1]).all()
+    files = sorted(glob.glob(os.path.join(cfg.outdir, "*.LDASOUT_DOMAIN1")))
+    assert len(files) == 8
+    d = ncio.read_ldasout(files[-1], grid)
+    for i, name in enumerate(L.DIAG_OUT):
+        if name != "T2M":
+            assert bit_equal(d[i], g["diags"][-1][L.DIAG_FULL.index(name)]).all(), name
+    # netCDF restart half way, resumed by a fresh driver
+    a = driver.OfflineDriver.from_files(cfg, write=False).run(nsteps=40)
+    path = str(tmp_path / "RESTART.nc")
+    a.save_restart(path)
+    b = driver.OfflineDriver.from_files(cfg, init=path, write=False)
+    assert b.step_index == 40
+    b.run()
+    assert bit_equal(b.cs.state.cpu().numpy(), g["states"][-1]).all()
+
+
+def test_offline_cli_runs_a_netcdf_case(engine_lib, tmp_path):
+    """tools/make_offline_case.py writes static/init/LDASIN files for the
+    namelist; noahmp_offline.py (the run/main.py counterpart) runs them."""
+    import importlib.util
+    import sys
+    from noahmp_amd import ncio
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    nml = tmp_path / "case.nml"
+    text = open(os.path.join(root, "examples", "offline_case.nml")).read()
+    for k in ("geo_em.d01.nc", "init.nc", "ldasin", "ldasout", "restart"):
+        text = text.replace(f"'{k}'", f"'{tmp_path / k}'").replace(f'"{k}"', f'"{tmp_path / k}"')
+    nml.write_text(text)
+    sys.path.insert(0, os.path.join(root, "tools"))
+    import make_offline_case
+    make_offline_case.main([str(nml), "--ny", "4", "--nx", "8"])
+    spec = importlib.util.spec_from_file_location("noahmp_offline",
+                                                  os.path.join(root, "noahmp_offline.py"))
+    cli = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(cli)
+    assert cli.main([str(nml)]) == 0
+    files = sorted(glob.glob(str(tmp_path / "ldasout" / "*.LDASOUT_DOMAIN1")))
+    assert len(files) == 8
+    cfg = config.Config(str(nml))
+    from noahmp_amd.params import Params
+    grid, _, _ = ncio.read_static(cfg.constfile, Params.builtin().as_dict(), cfg.begdatetime)
+    d = ncio.read_ldasout(files[-1], grid)
+    assert d.shape == (L.NDIAG_OUT, 32) and np.isfinite(d).all()

@@ -1,0 +1,115 @@
+"""netCDF-3 files of the offline run (noahmp_amd/ncio.py): static grid, state
+(initialization / restart), LDASIN forcing, LDASOUT output -- host side only.
+
+The reference names these files in run/case.nml:2-11 but has no reader or
+writer; the round trips below pin our own layouts (HRLDAS conventions)."""
+import datetime
+
+import numpy as np
+import pytest
+
+from golden_io import load
+from noahmp_amd import cases, layout as L, ncio, timeman
+
+T0 = datetime.datetime(2000, 1, 1)
+
+
+def bits(a):
+    a = np.asarray(a)
+    return a.view(np.int32 if a.dtype == np.float32 else np.int64)
+
+
+def fixture_grid(n, shape=(5, 8), seed=0):
+    """A grid whose land mask has n points; lat/lon of the land points given later."""
+    rng = np.random.default_rng(seed)
+    mask = np.zeros(shape[0] * shape[1], bool)
+    mask[np.sort(rng.choice(mask.size, n, replace=False))] = True
+    return mask.reshape(shape)
+
+
+def grid_for(cols, shape=(5, 8), seed=0):
+    mask = fixture_grid(cols.n, shape, seed)
+    g0 = ncio.Grid(np.zeros(shape), np.zeros(shape), mask)
+    lat = g0.scatter(np.degrees(cols.static_f[L.STATIC_F.index("LAT")].astype(np.float64)), 0.0)
+    lon = g0.scatter(np.degrees(np.linspace(-2.0, 2.0, cols.n)), 0.0)
+    return ncio.Grid(lat, lon, mask)
+
+
+def test_static_round_trip(tmp_path, ref_params):
+    cols = cases.make_columns(32, "conus", ref_params, seed=4)
+    grid = grid_for(cols)
+    p = str(tmp_path / "geo_em.d01.nc")
+    ncio.write_static(p, cols, grid)
+    g2, sf, si = ncio.read_static(p, ref_params, T0)
+    assert g2.n == 32 and np.array_equal(g2.index, grid.index)
+    assert np.array_equal(bits(sf), bits(cols.static_f)), "static_f"
+    assert np.array_equal(si, cols.static_i), "static_i (IST/ICE derived from the table types)"
+
+
+def test_state_round_trip(tmp_path, ref_params):
+    cols = cases.make_columns(32, "mixed", ref_params, seed=5)
+    grid = grid_for(cols)
+    p = str(tmp_path / "init.nc")
+    t = datetime.datetime(2000, 3, 1, 6)
+    ncio.write_state(p, grid, cols.state, cols.isnow, t, step=17)
+    st, isn, t2, step = ncio.read_state(p, grid)
+    assert np.array_equal(bits(st), bits(cols.state)) and np.array_equal(isn, cols.isnow)
+    assert t2 == t and step == 17
+    st64 = cols.state.astype(np.float64)
+    ncio.write_state(p, grid, st64, cols.isnow, t)
+    assert np.array_equal(bits(ncio.read_state(p, grid, np.float64)[0]), bits(st64))
+
+
+def test_ldasin_round_trip_and_derived_fields(tmp_path, ref_params):
+    cols = cases.make_columns(32, "mixed", ref_params, seed=6, julian=0.0)
+    grid = grid_for(cols)
+    f = cases.forcing_step(cols, 0.25, 366, 0, seed=1)
+    d = tmp_path / "ldasin"
+    d.mkdir()
+    ncio.write_ldasin(ncio.ldasin_path(str(d), T0), grid, f, T0, extras=True)
+    prov = ncio.LdasinForcing(str(d), grid, T0, datetime.timedelta(hours=1))
+    got = prov(0, T0)
+    assert np.array_equal(bits(got), bits(f)), "LDASIN with extras reproduces the slice"
+    # held over the input interval: 00:45 reads the 00:00 file
+    assert prov.input_time(T0 + datetime.timedelta(minutes=45)) == T0
+    assert np.array_equal(bits(prov(3, T0 + datetime.timedelta(minutes=45))[:9]), bits(f[:9]))
+    # standard HRLDAS file (no extras): COSZ from the grid at the step time, CO2/O2 from PSFC
+    ncio.write_ldasin(ncio.ldasin_path(str(d), T0), grid, f, T0, extras=False)
+    t = T0 + datetime.timedelta(minutes=30)
+    g = ncio.LdasinForcing(str(d), grid, T0, datetime.timedelta(hours=1))(2, t)
+    cz = timeman.cosz(grid.lat_rad, grid.lon_rad, timeman.julian(t), 366).astype(np.float32)
+    assert np.array_equal(bits(g[L.FORCING.index("COSZ")]), bits(cz))
+    psfc = f[L.FORCING.index("PSFC")].astype(np.float64)
+    assert np.array_equal(bits(g[L.FORCING.index("CO2AIR")]), bits(np.float32(395e-6 * psfc)))
+    assert np.array_equal(g[L.FORCING.index("SFCPRS")], f[L.FORCING.index("PSFC")])
+    with pytest.raises(FileNotFoundError):
+        prov(8, T0 + datetime.timedelta(hours=2))
+
+
+def test_ldasout_round_trip(tmp_path, ref_params):
+    cols = cases.make_columns(32, "mixed", ref_params, seed=7)
+    grid = grid_for(cols)
+    diag = np.random.default_rng(0).normal(size=(L.NDIAG_OUT, 32)).astype(np.float32)
+    p = ncio.ldasout_path(str(tmp_path), T0)
+    ncio.write_ldasout(p, grid, diag, T0)
+    assert p.endswith("2000010100.LDASOUT_DOMAIN1")
+    assert np.array_equal(bits(ncio.read_ldasout(p, grid)), bits(diag))
+    raw = ncio.read_ldasin(p)
+    assert (raw["FSA"][~grid.mask] == ncio.FILL).all()
+
+
+def test_trajectory_fixture_fits_the_files(tmp_path):
+    """The inputs of the reference trajectory survive the netCDF layouts bit for
+    bit (what tests/test_gpu_driver.py::test_driver_from_netcdf_files runs)."""
+    g = load("traj_casenml.npz")
+    cols = cases.ColumnSet(g["static_f"], g["static_i"], g["state0"], g["isnow0"], *([None] * 7))
+    grid = grid_for(cols)
+    p = str(tmp_path / "geo.nc")
+    ncio.write_static(p, cols, grid)
+    _, sf, si = ncio.read_static(p, load_params_dict(), T0)
+    assert np.array_equal(bits(sf), bits(g["static_f"])) and np.array_equal(si, g["static_i"])
+
+
+def load_params_dict():
+    from noahmp_amd.params import Params
+    return Params.builtin().as_dict()
