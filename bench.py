@@ -80,7 +80,9 @@ def parse():
     ap.add_argument("--precision", type=int, default=4, choices=(4, 8))
     ap.add_argument("--math", default="ref", choices=("ref", "fast"))
     ap.add_argument("--dt", type=float, default=1800.0)
-    ap.add_argument("--out-every", type=int, default=2, help="output (diag) step interval")
+    ap.add_argument("--out-every", type=int, default=6,
+                    help="output (diag + all-gather) step interval; default 6 = run/case.nml's "
+                         "output_frequency '3 hour' at the bench's 1800-s step")
     ap.add_argument("--period", type=int, default=48, help="resident forcing slices (cycled)")
     ap.add_argument("--streams", type=int, default=2,
                     help="column ranges stepped on their own HIP streams (overlaps launch tails)")
@@ -223,6 +225,7 @@ def main():
                     tj.get("streams", 1) == len(ranges.ranges) and \
                     tj.get("math") == a.math and tj.get("kind", "mixed") == a.kind and \
                     tj.get("order", "as-generated") == a.order and \
+                    tj.get("out_every", 2) == a.out_every and \
                     tj.get("source_hash") == _build.source_hash() \
                     and os.environ.get("NOAHMP_ENGINE_LIB") is None:
                 traffic = tj.get("bytes_per_launch")

@@ -10,11 +10,11 @@ cd /tmp && export TMPDIR=/tmp
 for C in FETCH_SIZE WRITE_SIZE; do
   timeout -k 10 180 rocprofv3 --pmc $C --kernel-trace --output-format csv -d "$OUT/calib_$C" -o run -- "$R/tools/calib_copy" 4194304 3 > "$OUT/calib_$C.log" 2>&1
   rc=$?; echo "calib $C rc=$rc"; [ $rc -eq 0 ] || exit $rc
-  timeout -k 10 300 rocprofv3 --pmc $C --kernel-trace --output-format csv -d "$OUT/bench_$C" -o run -- python3 "$R/bench.py" --steps 4 --warmup 1 --no-cpu-baseline ${BENCH_ARGS:-} > "$OUT/bench_$C.log" 2>&1
+  timeout -k 10 300 rocprofv3 --pmc $C --kernel-trace --output-format csv -d "$OUT/bench_$C" -o run -- python3 "$R/bench.py" --steps 5 --warmup 1 --no-cpu-baseline ${BENCH_ARGS:-} > "$OUT/bench_$C.log" 2>&1
   rc=$?; echo "bench $C rc=$rc"; [ $rc -eq 0 ] || exit $rc
 done
 if [ "${VALU:-1}" = 1 ]; then
-  timeout -k 10 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVES SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR --kernel-trace --output-format csv -d "$OUT/bench_SQ" -o run -- python3 "$R/bench.py" --steps 4 --warmup 1 --no-cpu-baseline ${BENCH_ARGS:-} > "$OUT/bench_SQ.log" 2>&1
+  timeout -k 10 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVES SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR --kernel-trace --output-format csv -d "$OUT/bench_SQ" -o run -- python3 "$R/bench.py" --steps 5 --warmup 1 --no-cpu-baseline ${BENCH_ARGS:-} > "$OUT/bench_SQ.log" 2>&1
   rc=$?; echo "bench SQ rc=$rc"; [ $rc -eq 0 ] || exit $rc
 fi
 find "$OUT" -name "*.csv" | head -20

@@ -53,6 +53,9 @@ def main():
     streams = 2
     if "--streams" in sys.argv:
         streams = int(sys.argv[sys.argv.index("--streams") + 1])
+    out_every = 6
+    if "--out-every" in sys.argv:
+        out_every = int(sys.argv[sys.argv.index("--out-every") + 1])
     kind = "mixed"
     if "--kind" in sys.argv:
         kind = sys.argv[sys.argv.index("--kind") + 1]
@@ -71,6 +74,7 @@ def main():
     import noahmp_pkg  # noqa: F401
     from noahmp_amd import build
     res = {"source_hash": build.source_hash(), "ncol": ncol, "streams": streams, "kind": kind,
+           "out_every": out_every,
            "precision": 4, "math": "ref", "kernel": KERNEL, "dispatches": nb,
            "fetch_size_kb": bf, "write_size_kb": bw, "read_correction": rf,
            "write_correction": rw, "read_bytes": rd, "write_bytes": wr,
