@@ -19,7 +19,7 @@ rc=$?; echo "bench rc=$rc"; tail -3 "$OUT/bench.log"; [ $rc -eq 0 ] || exit $rc
 
 if [ "${PROF:-1}" = 1 ]; then
   R=$PWD
-  (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/$OUT/prof" -o run -- python3 "$R/bench.py" --steps 10 --warmup 2 --no-cpu-baseline > "$R/$OUT/prof.log" 2>&1)
+  (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/$OUT/prof" -o run -- python3 "$R/bench.py" --no-cpu-baseline > "$R/$OUT/prof.log" 2>&1)
   rc=$?; echo "rocprof rc=$rc"; tail -3 "$OUT/prof.log"; [ $rc -eq 0 ] || exit $rc
   find "$OUT/prof" -name "*stats*" | head
 fi
