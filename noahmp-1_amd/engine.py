@@ -199,10 +199,15 @@ class StreamShards:
 
     def step(self, forcing: torch.Tensor, zsoil, dt: float, julian: float, yearlen: int,
              diag: torch.Tensor | None = None, diag_level: int = L.DIAG_NONE, events=None,
-             after: torch.cuda.Stream | None = None):
-        """One step of every range.  `after`: a stream whose pending work (e.g. the
-        forcing upload) each range waits for first; tensors from it are kept alive
-        until the ranges are done with them.  events: per-range (start, end) pairs."""
+             after: torch.cuda.Stream | None | str = "current"):
+        """One step of every range.  `after`: the stream whose pending work (the
+        forcing upload, a previous reader of `diag`) each range waits for first
+        -- by default the caller's current stream, where torch enqueues uploads;
+        tensors are kept alive until the ranges are done with them.  Pass None
+        only when the inputs are known to be complete (e.g. after a synchronize).
+        events: per-range (start, end) pairs."""
+        if after == "current":
+            after = torch.cuda.current_stream(self.streams[0].device)
         for i, (st, rng) in enumerate(zip(self.streams, self.ranges)):
             if after is not None:
                 st.wait_stream(after)

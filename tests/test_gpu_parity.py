@@ -387,3 +387,52 @@ def test_sflx_columns_rejects_what_the_kernel_cannot_honour(engines):
     with pytest.raises(_lib.NmpError):
         eng.sflx_columns(r)
     assert eng.sflx_columns(mk()) is not None
+
+
+@pytest.mark.parametrize("kind,ncol,opt_veg,precision", [
+    ("mixed", 1 << 20, 1, 4),          # config #3 as the bench runs it
+    ("global", 1_036_800, 2, 4),       # config #5 grid + carbon, fp32
+    ("global", 1_036_800, 2, 8),       # config #5 in fp64 (vs the fp64 restatement)
+])
+def test_full_size_sample_vs_oracle(engines, oracle_port, kind, ncol, opt_veg, precision):
+    """BASELINE sizes: two steps of every column on the GPU, then a seeded
+    sample of 2,048 columns re-run through the C restatement (bit-exact to the
+    reference in fp32 on every fixture): bit-identical in fp32, |d| <= 1e-9
+    (1 + |x|) in fp64.  Column independence makes the sample a full check of
+    those columns at full launch size (grid, stream ranges, ragged tail)."""
+    from noahmp_amd.engine import ColumnState, StreamShards
+    from noahmp_amd.params import Params
+    P = Params.builtin()
+    opts = dict(L.CASE_NML_OPTIONS, opt_veg=opt_veg)
+    eng = engines([opts[k] for k in L.OPTION_NAMES], precision)
+    dtype = torch.float32 if precision == 4 else torch.float64
+    cols = cases.make_columns(ncol, kind, P.as_dict(), seed=11, julian=150.0)
+    dt, jul = 1800.0, [150.0, 150.0 + 1800.0 / 86400.0]
+    F = [cases.forcing_step(cols, j, 366, s, seed=11) for s, j in enumerate(jul)]
+    cs = ColumnState.from_host(cols, DEV, dtype)
+    sh = StreamShards(eng, cs, 2)
+    diag = torch.zeros((L.NDIAG_OUT, ncol), dtype=dtype, device=DEV)
+    for s in range(2):
+        sh.step(torch.as_tensor(F[s], device=DEV).to(dtype), cases.CASE_NML_ZSOIL, dt, jul[s], 366,
+                diag if s == 1 else None, L.DIAG_OUT_LEVEL if s == 1 else L.DIAG_NONE)
+    sh.join()
+    torch.cuda.synchronize()
+    idx = np.sort(np.random.default_rng(3).choice(ncol, 2048, replace=False))
+    idx[-1] = ncol - 1  # the ragged tail's last column
+    st, isn = cols.state[:, idx], cols.isnow[idx]
+    for s in range(2):
+        st, isn, dg, status = oracle_port.step(
+            load_params(), tuple(opts[k] for k in L.OPTION_NAMES), cases.CASE_NML_ZSOIL, dt, 366,
+            jul[s], st, isn, cols.static_f[:, idx], cols.static_i[:, idx], F[s][:, idx],
+            precision=precision)
+    got = cs.state.cpu().numpy()[:, idx]
+    gd = diag.cpu().numpy()[:, idx]
+    od = np.stack([dg[L.DIAG_FULL.index(n)] for n in L.DIAG_OUT if n != "T2M"])
+    gd = np.stack([gd[i] for i, n in enumerate(L.DIAG_OUT) if n != "T2M"])
+    assert np.array_equal(cs.isnow.cpu().numpy()[idx], isn)
+    if precision == 4:
+        ok = bit_equal(got, st).all(0) & bit_equal(gd, od).all(0)
+        assert ok.all(), f"{(~ok).sum()} of {idx.size} sampled columns differ"
+    else:
+        ok = close(got, st, 1e-9, 1e-9).all(0) & close(gd, od, 1e-9, 1e-9).all(0)
+        assert ok.mean() >= 0.99, column_mismatch(got, st, 1e-9, 1e-9, STATE_NAMES)[1][:8]
