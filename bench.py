@@ -7,10 +7,11 @@ soil colours, ISNOW uniform in {0,-1,-2,-3}, dynamic vegetation off
 (case.nml options), fp32.  One bench step = one noahmp_sflx time step of
 every column (one kernel launch, state resident in HBM); every
 --out-every'th step also writes the 16 output diagnostics and, for N > 1,
-all-gathers them across ranks (RCCL over xGMI) on a side stream.
+gathers them to rank 0, the writing rank (RCCL over xGMI, --gather root; or
+all-gathers them to every rank with --gather all) on a side stream.
 
 Multi-GPU: one process per GPU (torchrun), columns statically sharded with
-no data-path collective other than that diagnostics all-gather; per-GPU work
+no data-path collective other than that diagnostics gather; per-GPU work
 is fixed (weak scaling).
 
 Prints one JSON line (rank 0) with the driver contract fields plus
@@ -83,6 +84,10 @@ def parse():
     ap.add_argument("--out-every", type=int, default=6,
                     help="output (diag + all-gather) step interval; default 6 = run/case.nml's "
                          "output_frequency '3 hour' at the bench's 1800-s step")
+    ap.add_argument("--gather", default="root", choices=("root", "all"),
+                    help="output-step diagnostics collective for N > 1: 'root' gathers to rank 0, "
+                         "the rank that writes LDASOUT (what the offline driver does); 'all' "
+                         "all-gathers to every rank")
     ap.add_argument("--period", type=int, default=48, help="resident forcing slices (cycled)")
     ap.add_argument("--streams", type=int, default=2,
                     help="column ranges stepped on their own HIP streams (overlaps launch tails)")
@@ -150,8 +155,10 @@ def main():
         F[s].copy_(torch.from_numpy(cases.forcing_step(
             cols, julian0 + s * a.dt / 86400.0, yearlen, s, seed=seed)))
     diag = [torch.zeros((L.NDIAG_OUT, n), dtype=dtype, device=dev) for _ in range(2)]
-    gathered = [torch.empty((world * L.NDIAG_OUT, n), dtype=dtype, device=dev) for _ in range(2)] \
-        if use_dist else None
+    gather_dst = 0 if a.gather == "root" else None
+    receives = use_dist and (gather_dst is None or rank == gather_dst)
+    gathered = [torch.empty((world * L.NDIAG_OUT, n), dtype=dtype, device=dev) if receives
+                else None for _ in range(2)]
     pending = [None, None]
     ranges = StreamShards(eng, cs, a.streams)
     comm = torch.cuda.Stream(dev) if use_dist else None
@@ -173,7 +180,8 @@ def main():
         if out and use_dist:
             ranges.join(comm)
             with torch.cuda.stream(comm):
-                _, pending[b] = shard.gather_diag(diag[b], gathered[b], async_op=True)
+                _, pending[b] = shard.gather_diag(diag[b], gathered[b], async_op=True,
+                                                  dst=gather_dst)
         return out
 
     for k in range(a.warmup):
@@ -248,7 +256,8 @@ def main():
                        "ncol_total": world * n, "dt_s": a.dt, "out_every": a.out_every,
                        "math": a.math, "column_order": a.order,
                        "streams": len(ranges.ranges),
-                       "parallelism": f"column-shard x{world}"},
+                       "parallelism": f"column-shard x{world}",
+                       "gather": a.gather if use_dist else None},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": "sflx_step_kernel", "kernel_ms": kern_ms,

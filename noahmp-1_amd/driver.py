@@ -22,7 +22,7 @@ offline/noahmp_config.py has no time loop, forcing reader or writer, SURVEY
   directory (forcing), all netCDF-3 (ncio.py).
 
 Multi-rank: each rank drives its own column shard; at output steps the
-diagnostics are all-gathered (shard.gather_diag) and rank 0 writes them.
+diagnostics are gathered to rank 0 (shard.gather_diag, dst=0), which writes them.
 """
 from __future__ import annotations
 
@@ -152,7 +152,7 @@ class OfflineDriver:
             self.t, self.step_index = t1, self.step_index + 1
             if out and self.write:
                 self.ranges.join()
-                d = shard.gather_diag(self.diag) if dist.is_initialized() else self.diag
+                d = shard.gather_diag(self.diag, dst=0) if dist.is_initialized() else self.diag
                 if rank == 0:
                     os.makedirs(cfg.outdir, exist_ok=True)
                     if self.grid is not None:

@@ -30,7 +30,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, out_path):
+def _worker(rank, world, port, out_path, dst=None):
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     sys.path[:0] = [root, os.path.join(root, "oracle"), os.path.join(root, "tests")]
@@ -50,19 +50,26 @@ def _worker(rank, world, port, out_path):
                               g["forcing"][:, sl])
     idx = [L.DIAG_FULL.index(d) if d != "T2M" else L.DIAG_FULL.index("T2MV") for d in L.DIAG_OUT]
     local = torch.from_numpy(np.ascontiguousarray(dg[idx]))
-    out, work = sh.gather_diag(local, async_op=True)
+    out, work = sh.gather_diag(local, async_op=True, dst=dst)
     work.wait()
-    if rank == 0:
+    if dst is not None and rank != dst:
+        assert out is None  # gather to root: only dst receives
+    elif rank == (0 if dst is None else dst):
         np.save(out_path, out.numpy())
     dist.barrier()
     dist.destroy_process_group()
 
 
-def test_gloo_two_rank_gather_equals_single_rank(oracle_port, tmp_path):
+@pytest.mark.parametrize("dst", [None, 0, 1], ids=["all-gather", "gather-to-0", "gather-to-1"])
+def test_gloo_two_rank_gather_equals_single_rank(oracle_port, tmp_path, dst):
+    """All-gather (bench --gather all) and gather to one rank (the offline
+    writer's and the bench's default mode) both rebuild the single-rank
+    diagnostics."""
     from golden_io import load, load_params
     world, port = 2, _free_port()
     out_path = str(tmp_path / "gathered.npy")
-    mp.start_processes(_worker, args=(world, port, out_path), nprocs=world, start_method="spawn")
+    mp.start_processes(_worker, args=(world, port, out_path, dst), nprocs=world,
+                       start_method="spawn")
     got = np.load(out_path)
     g = load("single_casenml_mixed.npz")
     _, _, dg, _ = oracle_port.step(load_params(), tuple(g["options"]), g["zsoil"],
