@@ -144,8 +144,6 @@ def main():
 
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    if use_dist:
-        dist.init_process_group("nccl", device_id=dev)
     dtype = torch.float32 if a.precision == 4 else torch.float64
     eng = Engine(P, opt_dict, device=local, precision=a.precision, math=a.math)
     cs = ColumnState.from_host(cols, dev, dtype)
@@ -154,14 +152,22 @@ def main():
     for s in range(a.period):
         F[s].copy_(torch.from_numpy(cases.forcing_step(
             cols, julian0 + s * a.dt / 86400.0, yearlen, s, seed=seed)))
-    diag = [torch.zeros((L.NDIAG_OUT, n), dtype=dtype, device=dev) for _ in range(2)]
     gather_dst = 0 if a.gather == "root" else None
     receives = use_dist and (gather_dst is None or rank == gather_dst)
-    gathered = [torch.empty((world * L.NDIAG_OUT, n), dtype=dtype, device=dev) if receives
+    gathered = [torch.zeros((world * L.NDIAG_OUT, n), dtype=dtype, device=dev) if receives
                 else None for _ in range(2)]
+    # a receiving rank writes its diagnostics straight into its own slot of the
+    # gather buffer: the collective is then in place (no local 64 MB copy)
+    diag = [gathered[b][rank * L.NDIAG_OUT:(rank + 1) * L.NDIAG_OUT] if receives else
+            torch.zeros((L.NDIAG_OUT, n), dtype=dtype, device=dev) for b in range(2)]
     pending = [None, None]
     ranges = StreamShards(eng, cs, a.streams)
     comm = torch.cuda.Stream(dev) if use_dist else None
+    if use_dist:
+        # after the range streams exist: RCCL's communicator creates streams of
+        # its own, and created first they left the two ranges sharing one of
+        # the process's hardware queues (GPU_MAX_HW_QUEUES=4), serialising them
+        dist.init_process_group("nccl", device_id=dev)
     del cols
 
     def step(k, ev=None):
