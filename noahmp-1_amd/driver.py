@@ -133,6 +133,18 @@ class OfflineDriver:
             self.zsoil = [float(v) for v in z["zsoil"]]
 
     # ---- time loop -----------------------------------------------------------------
+    def _gather_out(self):
+        """Rank 0: the (NDIAG_OUT, world * n_local) diagnostics of the whole
+        column set, in global column order (shards are contiguous blocks of
+        equal size, shard.shard_range); other ranks: None."""
+        world = dist.get_world_size()
+        src = self.diag if dist.get_backend() != "gloo" else self.diag.cpu()  # gloo: host tensors
+        d = shard.gather_diag(src, dst=0)
+        if d is None:
+            return None
+        n = self.diag.shape[1]
+        return d.view(world, L.NDIAG_OUT, n).permute(1, 0, 2).reshape(L.NDIAG_OUT, world * n)
+
     def run(self, nsteps: int | None = None):
         cfg = self.cfg
         total = cfg.step_count() if nsteps is None else nsteps
@@ -152,7 +164,7 @@ class OfflineDriver:
             self.t, self.step_index = t1, self.step_index + 1
             if out and self.write:
                 self.ranges.join()
-                d = shard.gather_diag(self.diag, dst=0) if dist.is_initialized() else self.diag
+                d = self._gather_out() if dist.is_initialized() else self.diag
                 if rank == 0:
                     os.makedirs(cfg.outdir, exist_ok=True)
                     if self.grid is not None:
