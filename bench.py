@@ -146,6 +146,8 @@ def main():
     dev = torch.device("cuda", local)
     dtype = torch.float32 if a.precision == 4 else torch.float64
     eng = Engine(P, opt_dict, device=local, precision=a.precision, math=a.math)
+    from noahmp_amd import lib as _nlib
+    build_hash = _nlib.load().nmp_build_hash().decode()  # lib.load refuses a stale library
     cs = ColumnState.from_host(cols, dev, dtype)
     n = cs.ncol
     F = torch.empty((a.period, L.NFORCING, n), dtype=dtype, device=dev)
@@ -153,14 +155,6 @@ def main():
         F[s].copy_(torch.from_numpy(cases.forcing_step(
             cols, julian0 + s * a.dt / 86400.0, yearlen, s, seed=seed)))
     gather_dst = 0 if a.gather == "root" else None
-    receives = use_dist and (gather_dst is None or rank == gather_dst)
-    gathered = [torch.zeros((world * L.NDIAG_OUT, n), dtype=dtype, device=dev) if receives
-                else None for _ in range(2)]
-    # a receiving rank writes its diagnostics straight into its own slot of the
-    # gather buffer: the collective is then in place (no local 64 MB copy)
-    diag = [gathered[b][rank * L.NDIAG_OUT:(rank + 1) * L.NDIAG_OUT] if receives else
-            torch.zeros((L.NDIAG_OUT, n), dtype=dtype, device=dev) for b in range(2)]
-    pending = [None, None]
     ranges = StreamShards(eng, cs, a.streams)
     comm = torch.cuda.Stream(dev) if use_dist else None
     if use_dist:
@@ -168,27 +162,24 @@ def main():
         # its own, and created first they left the two ranges sharing one of
         # the process's hardware queues (GPU_MAX_HW_QUEUES=4), serialising them
         dist.init_process_group("nccl", device_id=dev)
+        # double-buffered output-step gather; a receiving rank's engine writes
+        # straight into its own slot of the gather buffer (no local copy)
+        gat = shard.DiagGather(L.NDIAG_OUT, world * n, dtype, dev, dst=gather_dst, comm=comm)
+        sched = shard.OutputSchedule(a.out_every, gat, streams=ranges.streams)
+    else:
+        gat = None
+        sched = shard.OutputSchedule(a.out_every, bufs=[
+            torch.zeros((L.NDIAG_OUT, n), dtype=dtype, device=dev) for _ in range(2)])
     del cols
 
     def step(k, ev=None):
         """Bench step k: every column range on its own stream (StreamShards), plus the
-        async diagnostics all-gather on output steps."""
-        out = (k + 1) % a.out_every == 0
-        b = (k // a.out_every) % 2
-        if out and pending[b] is not None:
-            for st in ranges.streams:  # the previous gather from this buffer is done
-                with torch.cuda.stream(st):
-                    pending[b].wait()
-            pending[b] = None
+        async diagnostics gather on output steps (shard.OutputSchedule)."""
+        d = sched.diag_for(k)
         ranges.step(F[k % a.period], cases.CASE_NML_ZSOIL, a.dt, julian0 + k * a.dt / 86400.0,
-                    yearlen, diag[b] if out else None,
-                    L.DIAG_OUT_LEVEL if out else L.DIAG_NONE, events=ev)
-        if out and use_dist:
-            ranges.join(comm)
-            with torch.cuda.stream(comm):
-                _, pending[b] = shard.gather_diag(diag[b], gathered[b], async_op=True,
-                                                  dst=gather_dst)
-        return out
+                    yearlen, d, L.DIAG_OUT_LEVEL if d is not None else L.DIAG_NONE, events=ev)
+        sched.finish(k, producers=ranges.streams)
+        return d is not None
 
     for k in range(a.warmup):
         step(k)
@@ -202,9 +193,8 @@ def main():
     t0 = time.perf_counter()
     for k in range(a.steps):
         outs += step(a.warmup + k, evs[k])
-    for p in pending:
-        if p is not None:
-            p.wait()
+    if gat is not None:
+        gat.wait_all()
     torch.cuda.synchronize(dev)
     if use_dist:
         dist.barrier()
@@ -270,7 +260,8 @@ def main():
                          "bytes_per_launch": bpl, "launches_per_step": len(ranges.ranges),
                          "step_ms": step_ms, "bytes_per_step": bps, "valu": valu},
             "cpu_baseline": cpu,
-            "checks": {"status_nonzero_cols": st_bad, "stc_finite": finite},
+            "checks": {"status_nonzero_cols": st_bad, "stc_finite": finite,
+                       "build_hash": build_hash},
         }
         print(json.dumps(line), flush=True)
     eng.close()

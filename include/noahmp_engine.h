@@ -302,6 +302,10 @@ int nmp_engine_info(const nmp_engine* eng, int* device, int* precision, nmp_opti
 void nmp_finalize(nmp_engine* eng);
 const char* nmp_strerror(int code);
 int nmp_abi_version(void);
+/* Hash of the sources and flags this library was compiled from
+ * (noahmp-1_amd/build.py source_hash()); the Python loader refuses a library
+ * whose hash differs from the sources beside it, so a stale .so never runs. */
+const char* nmp_build_hash(void);
 
 #ifdef __cplusplus
 }

@@ -14,7 +14,9 @@ PKG = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(PKG)
 CSRC = os.path.join(PKG, "csrc")
 LIB_DIR = os.path.join(PKG, "lib")
-LIB_PATH = os.environ.get("NOAHMP_ENGINE_LIB") or os.path.join(LIB_DIR, "libnoahmp_engine.so")
+DEFAULT_LIB_PATH = os.path.join(LIB_DIR, "libnoahmp_engine.so")
+# NOAHMP_ENGINE_LIB: a tuning variant (tools/build_variants.py), hash-checked only on request
+LIB_PATH = os.environ.get("NOAHMP_ENGINE_LIB") or DEFAULT_LIB_PATH
 SOURCES = ["engine.hip", "sflx_kernel.hip", "tables.cpp"]
 HEADERS = ["dev_params.h", "sflx_kargs.h", "sflx_math.h", "glibc_math.h"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
@@ -27,11 +29,12 @@ FLAGS = ["-O3", f"--offload-arch={ARCH}", "-fPIC", "-shared", "-std=c++17",
          "-mllvm", "-disable-machine-licm"]
 
 
-def source_hash() -> str:
+def source_hash(extra: tuple = ()) -> str:
     """Hash of every engine source + build flag: identifies the kernel a
-    measurement (profiles/traffic.json) was taken on."""
+    measurement (profiles/traffic.json) was taken on.  Compiled into the
+    library (nmp_build_hash), so a stale library is detected at load time."""
     import hashlib
-    h = hashlib.sha256(" ".join(FLAGS).encode())
+    h = hashlib.sha256(" ".join(FLAGS + list(extra)).encode())
     for p in sorted(SOURCES + HEADERS):
         with open(os.path.join(CSRC, p), "rb") as f:
             h.update(f.read())
@@ -40,22 +43,27 @@ def source_hash() -> str:
     return h.hexdigest()[:16]
 
 
-def _newest_input() -> float:
-    paths = [os.path.join(CSRC, s) for s in SOURCES + HEADERS]
-    paths.append(os.path.join(ROOT, "include", "noahmp_engine.h"))
-    paths.append(os.path.abspath(__file__))
-    return max(os.path.getmtime(p) for p in paths)
+def built_hash(path: str = LIB_PATH) -> str | None:
+    """The source hash compiled into the library at `path` (read from the file,
+    without loading it), or None if there is no library or no marker."""
+    if not os.path.exists(path):
+        return None
+    with open(path, "rb") as f:
+        data = f.read()
+    i = data.find(b"NMP_BUILD_HASH=")
+    return data[i + 15:i + 31].decode() if i >= 0 else None
 
 
 def build(force: bool = False, verbose: bool = True, out: str | None = None,
           extra: tuple = ()) -> str:
     """Build the engine library (default: LIB_PATH; `out`/`extra` for tuning variants)."""
     path = out or LIB_PATH
-    if not force and os.path.exists(path) and os.path.getmtime(path) >= _newest_input():
+    want = source_hash(extra)
+    if not force and built_hash(path) == want:
         return path
     os.makedirs(os.path.dirname(path), exist_ok=True)
     tmp = path + ".tmp"
-    cmd = [HIPCC, *FLAGS, *extra, "-I", os.path.join(ROOT, "include"), "-I", CSRC, "-o", tmp,
+    cmd = [HIPCC, *FLAGS, *extra, f'-DNMP_BUILD_HASH="{want}"', "-I", os.path.join(ROOT, "include"), "-I", CSRC, "-o", tmp,
            *[os.path.join(CSRC, s) for s in SOURCES]]
     if verbose:
         print("[noahmp build]", " ".join(cmd), flush=True)

@@ -113,6 +113,13 @@ extern "C" {
 
 int nmp_abi_version(void) { return NMP_ABI_VERSION; }
 
+#ifndef NMP_BUILD_HASH
+#define NMP_BUILD_HASH "unknown"
+#endif
+// the marker prefix lets build.py read the hash from the file without loading it
+static const char kBuildHash[] = "NMP_BUILD_HASH=" NMP_BUILD_HASH;
+const char* nmp_build_hash(void) { return kBuildHash + 15; }
+
 const char* nmp_strerror(int code) {
   switch (code) {
     case NMP_OK: return "ok";

@@ -21,8 +21,14 @@ offline/noahmp_config.py has no time loop, forcing reader or writer, SURVEY
   static file (grid, types), the initialization file (state) and the LDASIN
   directory (forcing), all netCDF-3 (ncio.py).
 
-Multi-rank: each rank drives its own column shard; at output steps the
-diagnostics are gathered to rank 0 (shard.gather_diag, dst=0), which writes them.
+Multi-rank: each rank drives its own column shard (shard.shard_range of the
+land points; `from_files` reads only its slice); at output steps the
+diagnostics are gathered to rank 0 (shard.DiagGather, dst=0, ragged shards
+allowed), which writes them for the whole grid.
+
+Forcing reaches the GPU through `ForcingUpload`: pinned, double-buffered
+host buffers copied on a copy stream, so the host builds step t+1's forcing
+while the GPU steps t.
 """
 from __future__ import annotations
 
@@ -50,6 +56,51 @@ class SyntheticForcing:
                                   seed=self.seed)
 
 
+class ForcingUpload:
+    """Pinned, double-buffered host->device forcing uploads on a copy stream.
+
+    `put(f)` copies the (12, n) host array into pinned buffer b, enqueues its
+    upload to device buffer b on the copy stream and returns that device
+    buffer; the caller's launches wait on `stream`.  Buffer b is reused two
+    puts later: the host side waits for b's previous upload to land, the copy
+    stream for the launches that read it (`consumed_by`)."""
+
+    def __init__(self, n: int, dtype, device, nbuf: int = 2):
+        dev = torch.device(device)
+        self.host = [torch.empty((L.NFORCING, n), dtype=dtype, pin_memory=True)
+                     for _ in range(nbuf)]
+        self.dev = [torch.empty((L.NFORCING, n), dtype=dtype, device=dev) for _ in range(nbuf)]
+        self.stream = torch.cuda.Stream(dev)
+        self.uploaded = [None] * nbuf
+        self.consumed = [()] * nbuf
+        self.count = 0
+
+    def put(self, f: np.ndarray) -> torch.Tensor:
+        b = self.count % len(self.host)
+        self.count += 1
+        if self.uploaded[b] is not None:
+            self.uploaded[b].synchronize()  # pinned buffer b is free again
+        self.host[b].numpy()[...] = f
+        for e in self.consumed[b]:
+            self.stream.wait_event(e)
+        with torch.cuda.stream(self.stream):
+            self.dev[b].copy_(self.host[b], non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(self.stream)
+        self.uploaded[b], self.consumed[b] = ev, ()
+        self._last = b
+        return self.dev[b]
+
+    def consumed_by(self, streams):
+        """The last put's device buffer is read by launches on `streams`."""
+        evs = []
+        for s in streams:
+            e = torch.cuda.Event()
+            e.record(s)
+            evs.append(e)
+        self.consumed[self._last] = tuple(evs)
+
+
 def _stamp(t: datetime.datetime) -> str:
     return t.strftime("%Y%m%d%H")
 
@@ -65,11 +116,22 @@ def _is_boundary(t: datetime.datetime, t0: datetime.datetime, every) -> bool:
     return (t - t0) % every == datetime.timedelta(0)
 
 
+def _global_count(n: int, dev) -> int:
+    """Sum of the ranks' column counts."""
+    on_host = dist.get_backend() == "gloo"
+    t = torch.tensor([n], dtype=torch.int64, device="cpu" if on_host else dev)
+    dist.all_reduce(t)
+    return int(t.item())
+
+
 class OfflineDriver:
     def __init__(self, cfg: Config, cols: cases.ColumnSet, device: int = 0,
                  params: Params | None = None, forcing=None, precision: int = 4,
                  math: str = "ref", zsoil=cases.CASE_NML_ZSOIL, write: bool = True,
                  streams: int = 2, grid: ncio.Grid | None = None):
+        """cols: this rank's columns (all of them on a single rank); under an
+        initialised process group they must be the rank's shard_range block of
+        the global column set."""
         self.cfg = cfg
         self.grid = grid
         self.engine = Engine(params or Params.builtin(), cfg.engine_options(), device, precision,
@@ -86,6 +148,15 @@ class OfflineDriver:
         self.step_index = 0
         self.write = write
         self.diag = torch.zeros((L.NDIAG_OUT, self.cs.ncol), dtype=self.dtype, device=self.dev)
+        self.upload = ForcingUpload(self.cs.ncol, self.dtype, self.dev)
+        self.gather = None
+        if dist.is_initialized():
+            total = _global_count(self.cs.ncol, self.dev)
+            self.gather = shard.DiagGather(L.NDIAG_OUT, total, self.dtype, self.dev, dst=0)
+            if self.gather.n_local != self.cs.ncol:
+                raise ValueError(f"rank {dist.get_rank()} holds {self.cs.ncol} columns, its "
+                                 f"shard_range block of {total} has {self.gather.n_local}")
+        self.n_out = 0
         self.written = []
 
     @classmethod
@@ -97,8 +168,14 @@ class OfflineDriver:
         P = params or Params.builtin()
         grid, sf, si = ncio.read_static(cfg.constfile, P.as_dict(), cfg.begdatetime)
         st, isn, t0, step = ncio.read_state(init or cfg.initfile, grid)
-        cols = cases.ColumnSet(sf, si, st, isn, grid.lon_rad, *([None] * 6))
-        forcing = ncio.LdasinForcing(cfg.indir, grid, cfg.begdatetime, cfg.input_interval)
+        sl = slice(0, grid.n)
+        if dist.is_initialized():  # this rank's block of the land points
+            s0, cnt = shard.shard_range(grid.n, dist.get_rank(), dist.get_world_size())
+            sl = slice(s0, s0 + cnt)
+        cols = cases.ColumnSet(sf[:, sl], si[:, sl], st[:, sl], isn[sl], grid.lon_rad[sl],
+                               *([None] * 6))
+        forcing = ncio.LdasinForcing(cfg.indir, grid, cfg.begdatetime, cfg.input_interval,
+                                     cols=sl)
         drv = cls(cfg, cols, device, P, forcing, grid=grid, **kw)
         drv.t, drv.step_index = t0, step
         return drv
@@ -133,18 +210,6 @@ class OfflineDriver:
             self.zsoil = [float(v) for v in z["zsoil"]]
 
     # ---- time loop -----------------------------------------------------------------
-    def _gather_out(self):
-        """Rank 0: the (NDIAG_OUT, world * n_local) diagnostics of the whole
-        column set, in global column order (shards are contiguous blocks of
-        equal size, shard.shard_range); other ranks: None."""
-        world = dist.get_world_size()
-        src = self.diag if dist.get_backend() != "gloo" else self.diag.cpu()  # gloo: host tensors
-        d = shard.gather_diag(src, dst=0)
-        if d is None:
-            return None
-        n = self.diag.shape[1]
-        return d.view(world, L.NDIAG_OUT, n).permute(1, 0, 2).reshape(L.NDIAG_OUT, world * n)
-
     def run(self, nsteps: int | None = None):
         cfg = self.cfg
         total = cfg.step_count() if nsteps is None else nsteps
@@ -155,16 +220,26 @@ class OfflineDriver:
                 break
             t0 = self.t
             t1 = t0 + cfg.timestep
-            out = _is_boundary(t1, cfg.begdatetime, out_every)
-            f = torch.as_tensor(self.forcing(self.step_index, t0), device=self.dev).to(self.dtype)
+            out = _is_boundary(t1, cfg.begdatetime, out_every) and self.write
+            f = self.upload.put(self.forcing(self.step_index, t0))
+            diag = self.diag
+            if out and self.gather is not None:
+                b = self.n_out % len(self.gather.bufs)
+                self.gather.release(b, self.ranges.streams)
+                diag = self.gather.local(b)
             self.ranges.step(f, self.zsoil, self.dt, timeman.julian(t0), timeman.yearlen(t0.year),
-                             self.diag if out else None,
-                             L.DIAG_OUT_LEVEL if out else L.DIAG_NONE,
-                             after=torch.cuda.current_stream(self.dev))
+                             diag if out else None, L.DIAG_OUT_LEVEL if out else L.DIAG_NONE,
+                             after=self.upload.stream)
+            self.upload.consumed_by(self.ranges.streams)
             self.t, self.step_index = t1, self.step_index + 1
-            if out and self.write:
-                self.ranges.join()
-                d = self._gather_out() if dist.is_initialized() else self.diag
+            if out:
+                if self.gather is not None:
+                    self.gather.start(b, producers=self.ranges.streams)
+                    d = self.gather.assemble(b)
+                    self.n_out += 1
+                else:
+                    self.ranges.join()
+                    d = self.diag
                 if rank == 0:
                     os.makedirs(cfg.outdir, exist_ok=True)
                     if self.grid is not None:

@@ -125,6 +125,10 @@ class Engine:
         if diag_level != L.DIAG_NONE:
             nd = L.NDIAG_FULL if diag_level == L.DIAG_FULL_LEVEL else L.NDIAG_OUT
             assert diag is not None and diag.shape == (nd, n) and diag.dtype == self.dtype
+            # raw pointers offset by `lo` with rows exactly n apart: a strided view
+            # would be written in the wrong places
+            assert diag.is_contiguous()
+            assert diag.device.type == "cuda" and diag.device.index == self.device, diag.device
         zs = (C.c_float * 4)(*[float(z) for z in zsoil])
         s = stream if stream is not None else torch.cuda.current_stream(self.device)
         _lib.check(self._lib.nmp_step(self._h, hi - lo, n, zs, float(dt), float(julian),

@@ -73,6 +73,17 @@ def load(build_if_missing: bool = False):
             raise RuntimeError(
                 f"noahmp engine library not built ({path}); run __graft_entry__.build() "
                 "or python noahmp-1_amd/build.py -- there is no CPU fallback")
+    if path == _build.DEFAULT_LIB_PATH or os.environ.get("NOAHMP_CHECK_HASH") == "1":
+        # the library must come from the sources beside it (a stale .so that
+        # travelled with the snapshot would otherwise run silently)
+        got, want = _build.built_hash(path), _build.source_hash()
+        if got != want:
+            if build_if_missing:
+                _build.build()
+            else:
+                raise RuntimeError(
+                    f"stale noahmp engine library {path}: built from sources {got}, the sources "
+                    f"here hash to {want}; rebuild with __graft_entry__.build()")
     lib = C.CDLL(path)
     vp, i32p, f32p = C.c_void_p, C.POINTER(C.c_int32), C.POINTER(C.c_float)
     lib.nmp_read_tables.argtypes = [C.c_char_p, C.c_char_p, C.c_char_p, C.POINTER(NmpParams)]
@@ -99,6 +110,7 @@ def load(build_if_missing: bool = False):
     lib.nmp_strerror.argtypes = [C.c_int]
     lib.nmp_strerror.restype = C.c_char_p
     lib.nmp_abi_version.restype = C.c_int
+    lib.nmp_build_hash.restype = C.c_char_p
     _lib = lib
     return lib
 
@@ -106,7 +118,7 @@ def load(build_if_missing: bool = False):
 EXPORTED_SYMBOLS = ["nmp_read_tables", "nmp_init", "nmp_step", "nmp_run", "nmp_run_out",
                     "nmp_state_from_aos", "nmp_sflx_columns", "nmp_sflx_column",
                     "nmp_engine_info", "nmp_set_math", "nmp_finalize", "nmp_strerror",
-                    "nmp_abi_version"]
+                    "nmp_abi_version", "nmp_build_hash"]
 
 
 class NmpError(RuntimeError):

@@ -277,8 +277,10 @@ class LdasinForcing:
     from the run's start), held constant over the input interval."""
 
     def __init__(self, indir: str, grid: Grid, begin: datetime.datetime,
-                 every: datetime.timedelta):
+                 every: datetime.timedelta, cols: slice | None = None):
+        """cols: the land-point block this rank steps (default: all of them)."""
         self.indir, self.grid, self.begin, self.every = indir, grid, begin, every
+        self.cols = cols if cols is not None else slice(0, grid.n)
         self._t, self._fields = None, None
 
     def input_time(self, t: datetime.datetime) -> datetime.datetime:
@@ -289,16 +291,17 @@ class LdasinForcing:
         ti = self.input_time(t)
         if ti != self._t:
             raw = read_ldasin(ldasin_path(self.indir, ti))
-            self._fields = {k: self.grid.columns(v) for k, v in raw.items()}
+            self._fields = {k: self.grid.columns(v)[self.cols] for k, v in raw.items()}
             self._t = ti
         fl = self._fields
-        n = self.grid.n
+        lat, lon = self.grid.lat_rad[self.cols], self.grid.lon_rad[self.cols]
+        n = lat.shape[0]
         f = np.empty((L.NFORCING, n), np.float32)
         for fld, var in LDASIN_MAP.items():
             f[L.FORCING.index(fld)] = fl[var]
         psfc = fl["PSFC"].astype(np.float64)
         f[L.FORCING.index("COSZ")] = fl["COSZ"] if "COSZ" in fl else timeman.cosz(
-            self.grid.lat_rad, self.grid.lon_rad, timeman.julian(t), timeman.yearlen(t.year))
+            lat, lon, timeman.julian(t), timeman.yearlen(t.year))
         f[L.FORCING.index("CO2AIR")] = fl["CO2AIR"] if "CO2AIR" in fl else 395.0e-6 * psfc
         f[L.FORCING.index("O2AIR")] = fl["O2AIR"] if "O2AIR" in fl else 0.209 * psfc
         return f

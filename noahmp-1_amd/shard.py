@@ -2,15 +2,21 @@
 diagnostics gather -- the path's only collective.
 
 Columns are independent (no halo), so rank r owns a contiguous block of the
-global column set; the diagnostics SoA of every rank (NDIAG_OUT x n_local) is
-all-gathered at output steps into (world x NDIAG_OUT x n_local).  On "nccl"
-(= RCCL on ROCm) this is one all_gather_into_tensor over xGMI; on "gloo" (CPU
-tests) the list form.  When only one rank consumes the output (the offline
-writer: rank 0 writes LDASOUT), ``dst`` turns it into a gather to that rank:
-every sender pushes its block point-to-point straight to ``dst`` over its own
-xGMI link instead of relaying through a ring, so total link traffic falls by
-the world size and the root's N-1 incoming links run in parallel (SURVEY.md 8e,
-"gather to root").
+global column set (`shard_range`; the first ncol % world ranks hold one
+column more).  At output steps the diagnostics SoA of every rank (nfield x
+n_local) is gathered.  On "nccl" (= RCCL on ROCm) this is one collective over
+xGMI; on "gloo" (CPU tests) the list form.  When only one rank consumes the
+output (the offline writer: rank 0 writes LDASOUT), ``dst`` turns it into a
+gather to that rank: every sender pushes its block point-to-point straight to
+``dst`` over its own xGMI link instead of relaying through a ring, so total
+link traffic falls by the world size and the root's N-1 incoming links run in
+parallel ("gather to root").
+
+Ragged shards: a collective moves equal-sized blocks, so every rank's block
+travels in a slot of nfield * max(n_local) elements.  A rank's (nfield,
+n_local) diagnostics are the contiguous prefix of its slot (rows n_local
+apart, the layout the engine writes), and `DiagGather.assemble` trims each
+slot back to its rank's columns.
 """
 from __future__ import annotations
 
@@ -28,11 +34,12 @@ def shard_range(ncol_total: int, rank: int, world: int) -> tuple[int, int]:
 
 def gather_diag(local: torch.Tensor, out: torch.Tensor | None = None, group=None,
                 async_op: bool = False, dst: int | None = None):
-    """All-gather a (nfield, n_local) diagnostics block from every rank into
-    out = (world * nfield, n_local) (rank-major).  Shards must be equal-sized.
+    """All-gather an equal-sized block (any shape) from every rank into
+    out = (world * local.shape[0], *local.shape[1:]) (rank-major).
 
     With ``dst`` (a global rank) only that rank receives: it gets ``out`` as
-    above, every other rank gets None (its ``out`` argument is ignored)."""
+    above, every other rank gets None (its ``out`` argument is ignored).
+    Ragged shards go through `DiagGather`, which pads them into equal slots."""
     world = dist.get_world_size(group)
     if dst is not None and dist.get_rank() != dst:
         work = dist.gather(local.contiguous(), None, dst=dst, group=group, async_op=async_op)
@@ -52,3 +59,151 @@ def gather_diag(local: torch.Tensor, out: torch.Tensor | None = None, group=None
     else:
         work = dist.all_gather_into_tensor(out, local.contiguous(), group=group, async_op=async_op)
     return (out, work) if async_op else out
+
+
+class DiagGather:
+    """Output-step diagnostics gather with ragged shards and `nbuf` buffers.
+
+    Each buffer is one flat slot per rank on the receiving rank(s) (dst, or
+    every rank for dst=None) and a single slot on a pure sender.  `local(b)`
+    is the (nfield, n_local) block this rank's engine writes for buffer b; on
+    a receiver it IS this rank's slot of the gather buffer, so the collective
+    copies nothing locally.  `start(b)` issues the asynchronous collective on
+    `comm` (a side stream on GPUs) once `producers` are done, `release(b)`
+    makes streams wait until buffer b may be overwritten, `assemble(b)` is the
+    receiver's (nfield, ncol_total) result in global column order.
+
+    On a gloo group with CUDA buffers the slot is staged through host memory
+    (gloo moves host tensors); the staging is synchronous."""
+
+    def __init__(self, nfield: int, ncol_total: int, dtype, device, dst: int | None = 0,
+                 nbuf: int = 2, group=None, comm: torch.cuda.Stream | None = None):
+        self.group = group
+        self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+        self.dst = dst
+        self.nfield = nfield
+        self.counts = [shard_range(ncol_total, r, self.world)[1] for r in range(self.world)]
+        self.n_local = self.counts[self.rank]
+        self.slot = nfield * max(max(self.counts), 1)
+        self.device = torch.device(device)
+        self.receives = dst is None or self.rank == dst
+        self.staged = dist.get_backend(group) == "gloo" and self.device.type == "cuda"
+        nslot = self.world if self.receives else 1
+        self.bufs = [torch.zeros(nslot * self.slot, dtype=dtype, device=self.device)
+                     for _ in range(nbuf)]
+        self.host = [torch.zeros(nslot * self.slot, dtype=dtype) for _ in range(nbuf)] \
+            if self.staged else None
+        self.comm = comm
+        self.pending = [None] * nbuf
+
+    def _slot(self, buf: torch.Tensor, r: int) -> torch.Tensor:
+        return buf[r * self.slot:(r + 1) * self.slot]
+
+    def local(self, b: int) -> torch.Tensor:
+        own = self._slot(self.bufs[b], self.rank if self.receives else 0)
+        return own[:self.nfield * self.n_local].view(self.nfield, self.n_local)
+
+    def start(self, b: int, producers=()):
+        """Issue the gather of buffer b after every stream in `producers` (e.g.
+        the StreamShards range streams that wrote local(b))."""
+        bufs = self.host if self.staged else self.bufs
+        if self.staged:
+            for s in producers:
+                torch.cuda.current_stream(self.device).wait_stream(s)
+            bufs[b].copy_(self.bufs[b])
+            self._issue(b, bufs[b], async_op=False)
+            if self.receives:
+                self.bufs[b].copy_(bufs[b])
+            return
+        if self.comm is not None:
+            for s in producers:
+                self.comm.wait_stream(s)
+            with torch.cuda.stream(self.comm):
+                self._issue(b, bufs[b], async_op=True)
+        else:
+            if self.device.type == "cuda":
+                for s in producers:
+                    torch.cuda.current_stream(self.device).wait_stream(s)
+            self._issue(b, bufs[b], async_op=True)
+
+    def _issue(self, b: int, buf: torch.Tensor, async_op: bool):
+        own = self._slot(buf, self.rank if self.receives else 0)
+        if self.receives:
+            parts = [self._slot(buf, r) for r in range(self.world)]
+            if self.dst is not None:
+                w = dist.gather(own, parts, dst=self.dst, group=self.group, async_op=async_op)
+            elif dist.get_backend(self.group) == "gloo":
+                w = dist.all_gather(parts, own, group=self.group, async_op=async_op)
+            else:
+                w = dist.all_gather_into_tensor(buf, own, group=self.group, async_op=async_op)
+        else:
+            w = dist.gather(own, None, dst=self.dst, group=self.group, async_op=async_op)
+        self.pending[b] = w if async_op else None
+
+    def release(self, b: int, streams=()):
+        """Make `streams` (default: the current stream) wait until the collective
+        that last used buffer b is done, so it can be written again."""
+        w = self.pending[b]
+        if w is None:
+            return
+        if streams and self.device.type == "cuda":
+            for s in streams:
+                with torch.cuda.stream(s):
+                    w.wait()
+        else:
+            w.wait()
+        self.pending[b] = None
+
+    def assemble(self, b: int) -> torch.Tensor | None:
+        """Receiver: (nfield, ncol_total) diagnostics of buffer b in global
+        column order (waits for its collective on the current stream); None on
+        a pure sender."""
+        self.release(b)
+        if not self.receives:
+            return None
+        blocks = [self._slot(self.bufs[b], r)[:self.nfield * c].view(self.nfield, c)
+                  for r, c in enumerate(self.counts)]
+        return torch.cat(blocks, dim=1)
+
+    def wait_all(self):
+        for b in range(len(self.bufs)):
+            self.release(b)
+
+
+class OutputSchedule:
+    """The output-step loop shared by bench.py and the offline driver.
+
+    Step k writes diagnostics when (k + 1) % out_every == 0, into buffer
+    (k // out_every) % nbuf, so output step j+1 fills the other buffer while
+    output step j's gather may still be in flight.  `diag_for(k)` returns the
+    block step k writes (None on plain steps), after making `streams` wait for
+    the collective that last used that buffer; `finish(k, producers)` starts the
+    gather of an output step once `producers` (the streams that wrote it) are
+    done.  Without a DiagGather (single rank) `bufs` are plain local blocks."""
+
+    def __init__(self, out_every: int, gather: DiagGather | None = None, bufs=None,
+                 streams=()):
+        assert out_every >= 1 and (gather is not None or bufs)
+        self.out_every, self.gather, self.bufs = out_every, gather, bufs
+        self.streams = list(streams)
+        self.nbuf = len(gather.bufs) if gather is not None else len(bufs)
+
+    def is_output(self, k: int) -> bool:
+        return (k + 1) % self.out_every == 0
+
+    def buffer(self, k: int) -> int:
+        return (k // self.out_every) % self.nbuf
+
+    def diag_for(self, k: int):
+        if not self.is_output(k):
+            return None
+        b = self.buffer(k)
+        if self.gather is None:
+            return self.bufs[b]
+        self.gather.release(b, self.streams)
+        return self.gather.local(b)
+
+    def finish(self, k: int, producers=()):
+        if self.is_output(k) and self.gather is not None:
+            self.gather.start(self.buffer(k), producers)

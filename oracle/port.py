@@ -16,7 +16,12 @@ from ref import PARAM_FLOAT_FIELDS, PARAM_INT_FIELDS, PARAM_SHAPES, NPARAM_F, NP
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIBS = {4: os.path.join(HERE, "build", "liboracle_f32.so"),
         8: os.path.join(HERE, "build", "liboracle_f64.so"),
-        "cr": os.path.join(HERE, "build", "liboracle_f32cr.so")}
+        "cr": os.path.join(HERE, "build", "liboracle_f32cr.so"),
+        "4s": os.path.join(HERE, "build", "liboracle_f32_stats.so"),
+        "8s": os.path.join(HERE, "build", "liboracle_f64_stats.so")}
+# trip counts recorded by the stats builds, per column (noahmp_oracle.c ITER_STAT)
+STAT_LOOPS = ("vege_flux Newton", "stomata bisection", "frh2o", "soilwater sub-steps",
+              "bare_flux Newton")
 NST, NSF, NSI, NFC, NDG = 56, 6, 6, 12, 58
 _libs = {}
 
@@ -45,15 +50,17 @@ def _lib(precision):
         if not available(precision):
             raise FileNotFoundError(f"{LIBS[precision]} missing (run make -C oracle port)")
         lib = C.CDLL(LIBS[precision])
-        rt = np.float64 if precision == 8 else np.float32
+        rt = np.float64 if precision in (8, "8s") else np.float32
         rp = np.ctypeslib.ndpointer(rt, flags="C_CONTIGUOUS")
         ip = np.ctypeslib.ndpointer(np.int32, flags="C_CONTIGUOUS")
-        creal = C.c_double if precision == 8 else C.c_float
+        creal = C.c_double if precision in (8, "8s") else C.c_float
         lib.oracle_sflx_batch.argtypes = [C.c_int32, creal, C.c_int32, creal, rp, rp, ip, rp, ip,
                                           rp, rp, ip, C.c_char_p, C.c_void_p]
         lib.oracle_sflx_run.argtypes = [C.c_int32, C.c_int32, creal, C.c_int32, creal, rp, rp, ip,
                                         rp, ip, rp, C.c_int32, rp, ip, C.c_char_p, C.c_void_p]
-        assert lib.oracle_real_bytes() == (4 if precision == "cr" else precision)
+        assert lib.oracle_real_bytes() == (8 if precision in (8, "8s") else 4)
+        if precision in ("4s", "8s"):
+            lib.oracle_set_stats.argtypes = [C.c_void_p]
         _libs[precision] = (lib, rt)
     return _libs[precision]
 
@@ -79,9 +86,28 @@ def step(P: dict, options, zsoil, dt, yearlen, julian, state, isnow, static_f, s
     return st.T.copy(), isn, dg.T.copy(), status
 
 
-def run(P: dict, options, zsoil, dt, yearlen, julian0, state, isnow, static_f, static_i,
-        forcings, nsteps: int, precision: int = 4):
-    """nsteps steps over a forcing cycle forcings[(period, 12, n)] (timed CPU baseline)."""
+def step_stats(P: dict, options, zsoil, dt, yearlen, julian, state, isnow, static_f, static_i,
+               forcing, precision=4):
+    """step() through the trip-count build of `precision` (4 or 8): returns
+    step()'s tuple plus an (n, 5) int32 array of loop trip counts (STAT_LOOPS)."""
+    key = {4: "4s", 8: "8s"}[precision]
+    lib, _ = _lib(key)
+    n = isnow.shape[0]
+    buf = np.zeros((n, 8), np.int32)
+    lib.oracle_set_stats(buf.ctypes.data)
+    try:
+        out = step(P, options, zsoil, dt, yearlen, julian, state, isnow, static_f, static_i,
+                   forcing, precision=key)
+    finally:
+        lib.oracle_set_stats(None)
+    return (*out, buf[:, :len(STAT_LOOPS)].copy())
+
+
+def prepare_run(P: dict, options, zsoil, dt, yearlen, julian0, state, isnow, static_f, static_i,
+                forcings, nsteps: int, precision: int = 4):
+    """run() split in two: the host transposes happen here, the returned
+    callable is only the library's time loop (the CPU baseline times that) and
+    returns (state', isnow', diag, status) of the last step."""
     lib, rt = _lib(precision)
     n = isnow.shape[0]
     st = np.ascontiguousarray(np.asarray(state, rt).T)
@@ -92,7 +118,18 @@ def run(P: dict, options, zsoil, dt, yearlen, julian0, state, isnow, static_f, s
     dg = np.zeros((n, NDG), rt)
     status = np.zeros(n, np.int32)
     opts = (C.c_int32 * 12)(*[int(x) for x in options])
-    lib.oracle_sflx_run(n, nsteps, dt, int(yearlen), julian0, np.ascontiguousarray(zsoil, rt), st,
-                        isn, sf, si, fc, fc.shape[0], dg, status, pack_params(P),
-                        C.addressof(opts))
-    return st.T.copy(), isn, dg.T.copy(), status
+    zs = np.ascontiguousarray(zsoil, rt)
+    packed = pack_params(P)
+
+    def go():
+        lib.oracle_sflx_run(n, nsteps, dt, int(yearlen), julian0, zs, st, isn, sf, si, fc,
+                            fc.shape[0], dg, status, packed, C.addressof(opts))
+        return st.T.copy(), isn, dg.T.copy(), status
+    return go
+
+
+def run(P: dict, options, zsoil, dt, yearlen, julian0, state, isnow, static_f, static_i,
+        forcings, nsteps: int, precision: int = 4):
+    """nsteps steps over a forcing cycle forcings[(period, 12, n)]."""
+    return prepare_run(P, options, zsoil, dt, yearlen, julian0, state, isnow, static_f, static_i,
+                       forcings, nsteps, precision)()

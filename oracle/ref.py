@@ -75,6 +75,9 @@ def _load():
         lib.ref_dump_params.argtypes = [f32p, C.c_int32, i32p, C.c_int32]
         lib.ref_sflx_batch.argtypes = [C.c_int32, C.c_float, C.c_int32, C.c_float, f32p,
                                        f32p, i32p, f32p, i32p, f32p, f32p, i32p]
+        if hasattr(lib, "ref_sflx_run"):
+            lib.ref_sflx_run.argtypes = [C.c_int32, C.c_int32, C.c_float, C.c_int32, C.c_float,
+                                         f32p, f32p, i32p, f32p, i32p, f32p, C.c_int32, f32p, i32p]
         _lib = lib
     return _lib
 
@@ -132,3 +135,29 @@ def step(zsoil, dt, yearlen, julian, state, isnow, static_f, static_i, forcing):
         lib.ref_sflx_batch(n, float(dt), int(yearlen), float(julian),
                            np.ascontiguousarray(zsoil, np.float32), st, isn, sf, si, fc, dg, status)
     return st.T.copy(), isn, dg.T.copy(), status
+
+
+class Records:
+    """Column records in the harness layout (one column's fields contiguous),
+    transposed once, so a timed loop can call `run` without host transposes."""
+
+    def __init__(self, state, isnow, static_f, static_i, forcings):
+        self.st = np.ascontiguousarray(np.asarray(state, np.float32).T)
+        self.isn = np.ascontiguousarray(isnow, np.int32).copy()
+        self.sf = np.ascontiguousarray(np.asarray(static_f, np.float32).T)
+        self.si = np.ascontiguousarray(np.asarray(static_i, np.int32).T)
+        self.fc = np.ascontiguousarray(np.asarray(forcings, np.float32).transpose(0, 2, 1))
+        n = self.isn.shape[0]
+        self.dg = np.zeros((n, NDG), np.float32)
+        self.status = np.zeros(n, np.int32)
+
+
+def run(zsoil, dt, yearlen, julian0, rec: Records, nsteps: int):
+    """nsteps reference steps of `rec` in place (ref_sflx_run: the time loop in
+    the Fortran harness, forcing cycled over rec.fc's period)."""
+    lib = _load()
+    with _lock:
+        lib.ref_sflx_run(rec.isn.shape[0], int(nsteps), float(dt), int(yearlen), float(julian0),
+                         np.ascontiguousarray(zsoil, np.float32), rec.st, rec.isn, rec.sf, rec.si,
+                         rec.fc, rec.fc.shape[0], rec.dg, rec.status)
+    return rec

@@ -180,6 +180,28 @@ contains
     end do
   end subroutine ref_sflx_batch
 
+  ! nsteps steps over a forcing cycle fc(:, :, period) with the records kept in
+  ! the harness layout between steps (the CPU baseline's timed loop: no
+  ! per-step host transposes).  julian advances by dt/86400 per step.
+  subroutine ref_sflx_run(n, nsteps, dt, yearlen, julian0, zsoil, st, isnow, sf, si, fc, period, &
+       & dg, status) bind(C, name='ref_sflx_run')
+    integer(c_int32_t), value :: n, nsteps, yearlen, period
+    real(c_float), value :: dt, julian0
+    real(c_float), intent(in) :: zsoil(4)
+    real(c_float), intent(inout) :: st(NST, n)
+    integer(c_int32_t), intent(inout) :: isnow(n)
+    real(c_float), intent(in) :: sf(NSF, n)
+    integer(c_int32_t), intent(in) :: si(NSI, n)
+    real(c_float), intent(in) :: fc(NFC, n, period)
+    real(c_float), intent(out) :: dg(NDG, n)
+    integer(c_int32_t), intent(out) :: status(n)
+    integer :: s
+    do s = 0, nsteps - 1
+       call ref_sflx_batch(n, dt, yearlen, julian0 + real(s) * dt / 86400.0, zsoil, st, isnow, &
+            & sf, si, fc(:, :, mod(s, period) + 1), dg, status)
+    end do
+  end subroutine ref_sflx_run
+
   subroutine one_column(c, dt, yearlen, julian, zsoil_in, s, isn, sf, si, fc, d, stat)
     integer, intent(in) :: c, yearlen
     real, intent(in) :: dt, julian

@@ -31,7 +31,7 @@ def pytest_configure(config):
 def oracle_port():
     """The C restatement (oracle/build/liboracle_f{32,64}.so), built on demand with gcc."""
     import port
-    if not (port.available(4) and port.available(8) and port.available("cr")):
+    if not all(port.available(p) for p in port.LIBS):
         subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle"), "port"], check=True)
     return port
 

@@ -112,3 +112,66 @@ def parity_vs_reference(st, isn, dg, status, g, state_key="state1", diag_key="di
         _, rep_d = column_mismatch(dg[:, ~tie], edg[:, ~tie], *DIAG_LOOSE)
         msg.append("loose-envelope misses: " + "; ".join(rep_s[:6] + rep_d[:6]))
     return r, " | ".join(msg)
+
+
+# fp64 engine vs the fp32 reference ("fp64 build vs fp32 oracle:
+# same thresholds x10").  The reference cannot be built in fp64 (H11,
+# core/module_noahmp_func.f90:392-393, :442, :2765), so the fp64 path is held
+# to the fp32 reference with the tolerances widened tenfold.  Residual misses
+# are columns whose Newton/bisection loops exit on a different iteration in
+# fp64 than in fp32 (the exit tests compare against fixed thresholds, e.g.
+# vege_flux :2870-2875); tests/test_oracle_golden.py pins that explanation with
+# the oracle's trip-count builds.  Status: the energy/radiation balance checks
+# (ERRSW/ERRENG, :688-721) fire on fp32 round-off of ~1e3 W/m2 terms against a
+# 0.01 W/m2 threshold, so only the hard-stop bits are compared in fp64.
+FP64_STATE_TOL = (1e-4, 1e-3)   # x10 of STATE_TOL
+FP64_DIAG_TOL = (1e-3, 1e-1)    # x10 of DIAG_TOL
+FP64_STATE_ENV = (1e-2, 1e-2)   # envelope for the loop-exit residuals
+FP64_DIAG_ENV = (5e-2, 2.0)
+FP64_TOL_FRAC = 0.97            # per fixture, non-tie columns inside the x10 bar
+FP64_POOLED_FRAC = 0.985        # pooled over every fixture
+HARD_STATUS = 4 | 8 | 16 | 64 | 128   # FIRE, HCAN, ZLVL, OPTVEG, STOP
+
+
+def parity_fp64_vs_reference(st, isn, dg, status, g, state_key="state1", diag_key="diag",
+                             isnow_key="isnow1", status_key="status"):
+    """fp64 result vs an fp32 reference fixture at SURVEY 8c's x10 bar.
+
+    Returns (summary dict, per-column miss mask of non-tie columns outside the
+    x10 bar, per-column envelope-miss mask, field report of the misses)."""
+    est, edg = g[state_key], g[diag_key]
+    hard = lambda s: as_ref_status(s) & HARD_STATUS
+    tie = (isn != g[isnow_key]) | (hard(status) != hard(g[status_key]))
+    tight = close(st, est, *FP64_STATE_TOL).all(0) & close(dg, edg, *FP64_DIAG_TOL).all(0)
+    env = close(st, est, *FP64_STATE_ENV).all(0) & close(dg, edg, *FP64_DIAG_ENV).all(0)
+    miss = ~tight & ~tie
+    env_miss = ~env & ~tie
+    nt = max(int((~tie).sum()), 1)
+    r = dict(n=int(isn.size), nontie=int((~tie).sum()), tight=int((tight & ~tie).sum()),
+             frac=float((tight & ~tie).sum() / nt), miss=int(miss.sum()),
+             env_miss=int(env_miss.sum()), tie=int(tie.sum()))
+    rep = []
+    if miss.any():
+        from noahmp_amd import layout as L
+        names = [f"{n}[{k}]" if w > 1 else n for n, w in L.STATE_FIELDS for k in range(w)]
+        rep = (column_mismatch(st[:, miss], est[:, miss], *FP64_STATE_TOL, names)[1]
+               + column_mismatch(dg[:, miss], edg[:, miss], *FP64_DIAG_TOL, L.DIAG_FULL)[1])
+    return r, miss, env_miss, rep
+
+
+def check_fp64_trajectory_step(name, s, st, isn, dg, g, k):
+    """Shared by the CPU (fp64 restatement) and GPU (fp64 engine) trajectory tests."""
+    from noahmp_amd import layout as L
+    exp, edg = g["states"][k], g["diags"][k]
+    ok = close(st, exp, 1e-3, 1e-3).all(0) & close(dg, edg, 1e-3, 1e-1).all(0) & \
+        (isn == g["isnows"][k])
+    if name == "snow":
+        for f in ("SNEQV", "SNOWH"):
+            a, b = st[L.si(f)].mean(), exp[L.si(f)].mean()
+            assert abs(a - b) <= 0.01 * abs(b) + 1e-3, (s, f, a, b)
+        assert abs((isn < 0).mean() - (g["isnows"][k] < 0).mean()) <= 0.01 + 1.0 / isn.size
+    else:
+        if name == "casenml":
+            assert ok[0], (name, s, "the run/case.nml column is outside the x10 trajectory bar")
+        assert ok.mean() >= 0.9, (name, s, ok.mean())
+    return float(ok.mean())

@@ -222,3 +222,29 @@ def test_kernel_emits_every_output_once():
     stored = set(re.findall(r"out\.s\(NMP_S_(\w+)", src)) | set(
         re.findall(r"so\[\(?NMP_S_(\w+)", src))
     assert {n for n, _ in L.STATE_FIELDS} <= stored
+
+
+def test_library_carries_its_source_hash(engine_lib):
+    """Build provenance: the library reports the hash of the sources it was
+    compiled from, and it is the hash of the sources in this tree."""
+    from noahmp_amd import build
+    assert engine_lib.nmp_build_hash().decode() == build.source_hash()
+    assert build.built_hash() == build.source_hash()
+
+
+def test_stale_library_is_refused(tmp_path, monkeypatch):
+    """A library whose embedded hash differs from the sources is refused by
+    lib.load() (no silent run of a stale kernel)."""
+    import importlib
+    from noahmp_amd import build
+    lib_mod = importlib.import_module("noahmp_amd.lib")
+    stale = tmp_path / "libnoahmp_engine.so"
+    data = open(build.DEFAULT_LIB_PATH, "rb").read()
+    i = data.find(b"NMP_BUILD_HASH=") + 15
+    stale.write_bytes(data[:i] + b"0123456789abcdef" + data[i + 16:])
+    assert build.built_hash(str(stale)) == "0123456789abcdef"
+    monkeypatch.setattr(build, "LIB_PATH", str(stale))
+    monkeypatch.setattr(build, "DEFAULT_LIB_PATH", str(stale))
+    monkeypatch.setattr(lib_mod, "_lib", None)
+    with pytest.raises(RuntimeError, match="stale"):
+        lib_mod.load()

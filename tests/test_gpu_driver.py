@@ -126,3 +126,75 @@ def test_offline_cli_runs_a_netcdf_case(engine_lib, tmp_path):
     grid, _, _ = ncio.read_static(cfg.constfile, Params.builtin().as_dict(), cfg.begdatetime)
     d = ncio.read_ldasout(files[-1], grid)
     assert d.shape == (L.NDIAG_OUT, 32) and np.isfinite(d).all()
+
+
+def _write_netcdf_case(tmp_path, g):
+    """static / init / LDASIN files of the traj_casenml columns + a namelist (900-s steps)."""
+    from noahmp_amd import ncio
+    from test_config import write_case
+    from test_ncio import grid_for
+    cols = _cols(g)
+    grid = grid_for(cols)
+    static, init, indir = tmp_path / "geo_em.d01.nc", tmp_path / "init.nc", tmp_path / "ldasin"
+    indir.mkdir()
+    nml = write_case(tmp_path)
+    text = open(nml).read().replace("'geo_em.d01.nc'", f"'{static}'").replace(
+        '"init.nc"', f'"{init}"').replace("'ldasin'", f"'{indir}'").replace(
+        "'1 hour'", "'900 second'")
+    open(nml, "w").write(text)
+    cfg = config.Config(nml)
+    ncio.write_static(str(static), cols, grid)
+    ncio.write_state(str(init), grid, g["state0"], g["isnow0"], cfg.begdatetime)
+    for k, t in enumerate([cfg.begdatetime + i * cfg.timestep for i in range(96)]):
+        ncio.write_ldasin(ncio.ldasin_path(str(indir), t), grid, g["forcing"][k], t)
+    return nml, grid
+
+
+def _driver_rank(rank, world, port, nml, out_dir):
+    """One rank of a multi-rank offline run on the box's single GPU (gloo for
+    the gather: RCCL refuses several ranks on one device)."""
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    cfg = config.Config(nml)
+    drv = driver.OfflineDriver.from_files(cfg)
+    drv.run()
+    np.savez(os.path.join(out_dir, f"rank{rank}.npz"), state=drv.cs.state.cpu().numpy(),
+             isnow=drv.cs.isnow.cpu().numpy())
+    dist.barrier()
+    drv.engine.close()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_driver_multi_rank_files_equal_reference(engine_lib, tmp_path, world):
+    """OfflineDriver.from_files under a process group: each rank reads and
+    steps only its shard_range block of the 32 land points (ragged at world 3:
+    11/11/10), rank 0 gathers (shard.DiagGather) and writes LDASOUT for the
+    whole grid.  Every LDASOUT file and every rank's final state equal the
+    reference trajectory bit for bit."""
+    import socket
+    import torch.multiprocessing as mp
+    from noahmp_amd import ncio, shard
+    g = load("traj_casenml.npz")
+    nml, grid = _write_netcdf_case(tmp_path, g)
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    mp.start_processes(_driver_rank, args=(world, port, str(nml), str(tmp_path)), nprocs=world,
+                       start_method="spawn")
+    cfg = config.Config(str(nml))
+    files = sorted(glob.glob(os.path.join(cfg.outdir, "*.LDASOUT_DOMAIN1")))
+    assert len(files) == 8
+    for j, fn in enumerate(files):
+        d = ncio.read_ldasout(fn, grid)
+        k = (j + 1) * 12 - 1  # output every 3 hours = 12 steps of 900 s
+        for i, name in enumerate(L.DIAG_OUT):
+            if name != "T2M":
+                assert bit_equal(d[i], g["diags"][k][L.DIAG_FULL.index(name)]).all(), (fn, name)
+    for r in range(world):
+        s0, cnt = shard.shard_range(32, r, world)
+        with np.load(tmp_path / f"rank{r}.npz") as z:
+            assert z["state"].shape[1] == cnt
+            assert bit_equal(z["state"], g["states"][-1][:, s0:s0 + cnt]).all(), r
+            assert np.array_equal(z["isnow"], g["isnows"][-1][s0:s0 + cnt])

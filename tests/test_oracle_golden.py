@@ -8,8 +8,8 @@ order, same libm, no contraction.
 import numpy as np
 import pytest
 
-from golden_io import (as_ref_status, bit_equal, fixture_params, fixture_tags, load, load_params,
-                       single_names)
+from golden_io import (as_ref_status, bit_equal, check_fp64_trajectory_step, fixture_params,
+                       fixture_tags, load, load_params, single_names)
 from noahmp_amd import layout as L
 
 
@@ -74,19 +74,63 @@ def test_fixture_coverage():
     assert (t["isnows"] != t["isnows"][:1]).any(), "snow trajectory never changes layering"
 
 
-def test_fp64_restatement_tracks_fp32(oracle_port):
-    """The fp64 restatement (engine precision 8 oracle) stays near the fp32 reference."""
-    g = load("single_casenml_conus.npz")
+def test_fp64_restatement_vs_fp32_reference(oracle_port):
+    """The fp64 restatement (the fp64 engine's CPU twin) against the fp32
+    reference fixtures at SURVEY 8c's x10 bar, on all 56 state values and all
+    58 outputs of every single-call fixture (golden_io.parity_fp64_vs_reference).
+
+    The misses are explained, not just counted: the trip-count builds of the
+    oracle (port.step_stats) show that most columns outside the bar ran a
+    Newton/bisection loop for a different number of iterations in fp64 than
+    in fp32 (measured: 116 of 129 misses over the 14,080 columns; the rest
+    are EAH-only residuals of 1-5e-4 or columns whose vege_flux loop hit its
+    20-iteration cap in both precisions)."""
+    from golden_io import (FP64_POOLED_FRAC, FP64_TOL_FRAC, parity_fp64_vs_reference)
+    tot = dict(nontie=0, tight=0, miss=0, explained=0, env_miss=0)
+    for name in single_names():
+        g = load(f"single_{name}.npz")
+        args = (fixture_params(g), tuple(g["options"]), g["zsoil"], float(g["dt"]),
+                int(g["yearlen"]), float(g["julian"]), g["state0"], g["isnow0"], g["static_f"],
+                g["static_i"], g["forcing"])
+        *o32, it32 = oracle_port.step_stats(*args, precision=4)
+        assert bit_equal(o32[0], g["state1"]).all(), name  # the stats build is the oracle
+        *o64, it64 = oracle_port.step_stats(*args, precision=8)
+        r, miss, env_miss, rep = parity_fp64_vs_reference(*o64, g)
+        iterdiff = (it32 != it64).any(1)
+        capped = (it32[:, 0] >= 20) | (it64[:, 0] >= 20)
+        print(name, r, "misses with a trip-count difference:", int((miss & iterdiff).sum()))
+        assert r["frac"] >= FP64_TOL_FRAC, (name, r, rep[:8])
+        assert r["env_miss"] <= 1, (name, r)
+        for k in ("nontie", "tight", "miss", "env_miss"):
+            tot[k] += r[k]
+        tot["explained"] += int((miss & (iterdiff | capped)).sum())
+    print("pooled", tot)
+    assert tot["tight"] / tot["nontie"] >= FP64_POOLED_FRAC, tot
+    assert tot["explained"] >= 0.85 * tot["miss"], tot
+    assert tot["env_miss"] <= 2, tot
+
+
+@pytest.mark.parametrize("name", ["casenml", "combo_a", "snow"])
+def test_fp64_restatement_trajectory_vs_reference(oracle_port, name):
+    """fp64 trajectories vs the fp32 reference runs.  SURVEY 8c: 96-step
+    snow-free trajectory rel <= 1e-4, x10 for fp64 -> 1e-3 (fluxes: 1e-3 rel,
+    0.1 W/m2 floor); snow trajectories by distribution (domain means within 1 %).
+    The run/case.nml column (column 0) must meet the bar at every saved step."""
+    g = load(f"traj_{name}.npz")
     P = load_params()
-    st, isn, dg, status = oracle_port.step(P, tuple(g["options"]), g["zsoil"], float(g["dt"]),
-                                           int(g["yearlen"]), float(g["julian"]), g["state0"],
-                                           g["isnow0"], g["static_f"], g["static_i"], g["forcing"],
-                                           precision=8)
-    same = isn == g["isnow1"]
-    assert same.mean() > 0.99
-    stc = L.s("STC")
-    d = np.abs(st[stc][:, same] - g["state1"][stc][:, same])
-    assert np.nanpercentile(d, 99) < 1e-2
+    opts, dt, ylen, ke = tuple(g["options"]), float(g["dt"]), int(g["yearlen"]), int(g["keep_every"])
+    st, isn = g["state0"].astype(np.float64), g["isnow0"]
+    k = 0
+    for s in range(g["forcing"].shape[0]):
+        jul = float(g["julian0"]) + s * dt / 86400.0
+        st, isn, dg, _ = oracle_port.step(P, opts, g["zsoil"], dt, ylen, jul, st, isn,
+                                          g["static_f"], g["static_i"], g["forcing"][s],
+                                          precision=8)
+        if (s + 1) % ke == 0 or s == g["forcing"].shape[0] - 1:
+            fr = check_fp64_trajectory_step(name, s, st, isn, dg, g, k)
+            if s == g["forcing"].shape[0] - 1:
+                print(name, "columns inside the x10 bar at the last step:", fr)
+            k += 1
 
 
 @pytest.mark.parametrize("name", single_names())
@@ -102,3 +146,24 @@ def test_cr_math_restatement_meets_parity_bar(oracle_port, name):
     r, msg = parity_vs_reference(*out, g)
     assert not msg, msg
     assert r["exact"] > 0.7
+
+
+def test_reference_run_loop_equals_repeated_steps():
+    """ref.run (the time loop inside the Fortran harness, the CPU baseline's
+    timed call) == ref.step issued per step, bit for bit."""
+    import ref
+    if not ref.available():
+        pytest.skip("reference oracle not built (oracle/_ref)")
+    g = load("traj_casenml.npz")
+    ref.configure(tuple(g["options"]))
+    dt, jul0, ylen = float(g["dt"]), float(g["julian0"]), int(g["yearlen"])
+    F = g["forcing"][:5]
+    rec = ref.Records(g["state0"], g["isnow0"], g["static_f"], g["static_i"], F)
+    ref.run(g["zsoil"], dt, ylen, jul0, rec, 7)
+    st, isn = g["state0"], g["isnow0"]
+    for s in range(7):
+        jul = float(np.float32(jul0) + np.float32(s) * np.float32(dt) / np.float32(86400.0))
+        st, isn, dg, status = ref.step(g["zsoil"], dt, ylen, jul, st, isn, g["static_f"],
+                                       g["static_i"], F[s % 5])
+    assert bit_equal(rec.st.T, st).all() and np.array_equal(rec.isn, isn)
+    assert bit_equal(rec.dg.T, dg).all()

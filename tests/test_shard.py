@@ -1,7 +1,7 @@
-"""Multi-rank path on CPU (gloo, world_size 2): column sharding + the
-output-step diagnostics all-gather reproduce the single-rank result bit for
-bit (SURVEY.md 8e correctness test).  Per-shard physics is computed by the
-oracle restatement (this is a test of the sharding plumbing)."""
+"""Multi-rank path on CPU (gloo, world sizes 2 and 3, ragged shards): column
+sharding + the output-step diagnostics gather reproduce the single-rank
+result bit for bit (SURVEY.md 8e correctness test).  Per-shard physics is
+computed by the oracle restatement (this is a test of the sharding plumbing)."""
 import os
 import socket
 
@@ -30,61 +30,84 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, out_path, dst=None):
+def _oracle_steps(g, sl, nsteps):
+    """The oracle's diagnostics (DIAG_OUT fields) after each of nsteps steps of columns sl."""
+    import port as oracle
+    from golden_io import load_params
+    idx = [L.DIAG_FULL.index(d) if d != "T2M" else L.DIAG_FULL.index("T2MV") for d in L.DIAG_OUT]
+    st, isn, out = g["state0"][:, sl], g["isnow0"][sl], []
+    for k in range(nsteps):
+        st, isn, dg, _ = oracle.step(load_params(), tuple(g["options"]), g["zsoil"],
+                                     float(g["dt"]), int(g["yearlen"]),
+                                     float(g["julian"]) + k * float(g["dt"]) / 86400.0, st, isn,
+                                     g["static_f"][:, sl], g["static_i"][:, sl],
+                                     g["forcing"][:, sl])
+        out.append(np.ascontiguousarray(dg[idx]))
+    return out
+
+
+NSTEPS, OUT_EVERY = 8, 2   # 4 output steps: each of the 2 buffers is reused once
+
+
+def _worker(rank, world, port, out_path, ncol, dst=None):
+    """One rank of the bench/driver output loop (shard.OutputSchedule +
+    DiagGather) on gloo: steps its ragged shard (oracle physics), writes each
+    output step's diagnostics into the schedule's buffer, gathers them
+    asynchronously, and the receiver assembles every output step."""
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     sys.path[:0] = [root, os.path.join(root, "oracle"), os.path.join(root, "tests")]
     import noahmp_pkg  # noqa: F401
-    import port as oracle
-    from golden_io import load, load_params
+    from golden_io import load
     from noahmp_amd import shard as sh
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     g = load("single_casenml_mixed.npz")
-    n = g["isnow0"].shape[0]
-    s0, cnt = sh.shard_range(n, rank, world)
-    sl = slice(s0, s0 + cnt)
-    _, _, dg, _ = oracle.step(load_params(), tuple(g["options"]), g["zsoil"], float(g["dt"]),
-                              int(g["yearlen"]), float(g["julian"]), g["state0"][:, sl],
-                              g["isnow0"][sl], g["static_f"][:, sl], g["static_i"][:, sl],
-                              g["forcing"][:, sl])
-    idx = [L.DIAG_FULL.index(d) if d != "T2M" else L.DIAG_FULL.index("T2MV") for d in L.DIAG_OUT]
-    local = torch.from_numpy(np.ascontiguousarray(dg[idx]))
-    out, work = sh.gather_diag(local, async_op=True, dst=dst)
-    work.wait()
-    if dst is not None and rank != dst:
-        assert out is None  # gather to root: only dst receives
-    elif rank == (0 if dst is None else dst):
-        np.save(out_path, out.numpy())
+    s0, cnt = sh.shard_range(ncol, rank, world)
+    local = _oracle_steps(g, slice(s0, s0 + cnt), NSTEPS)
+    gat = sh.DiagGather(L.NDIAG_OUT, ncol, torch.float32, "cpu", dst=dst)
+    sched = sh.OutputSchedule(OUT_EVERY, gat)
+    got, prev = [], None
+    for k in range(NSTEPS):
+        d = sched.diag_for(k)
+        if d is not None:
+            assert d.shape == (L.NDIAG_OUT, cnt)
+            d.copy_(torch.from_numpy(local[k]))  # "the engine writes its block"
+        sched.finish(k)
+        if d is not None:
+            if prev is not None:  # the previous output step, assembled while this one flies
+                got.append(gat.assemble(prev))
+            prev = sched.buffer(k)
+    gat.wait_all()
+    got.append(gat.assemble(prev))
+    if gat.receives and rank == (0 if dst is None else dst):
+        np.save(out_path, torch.stack(got).numpy())
+    if not gat.receives:
+        assert all(x is None for x in got)
     dist.barrier()
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("dst", [None, 0, 1], ids=["all-gather", "gather-to-0", "gather-to-1"])
-def test_gloo_two_rank_gather_equals_single_rank(oracle_port, tmp_path, dst):
-    """All-gather (bench --gather all) and gather to one rank (the offline
-    writer's and the bench's default mode) both rebuild the single-rank
-    diagnostics."""
-    from golden_io import load, load_params
-    world, port = 2, _free_port()
+@pytest.mark.parametrize("world,ncol,dst", [(2, 2048, 0), (2, 2047, None), (3, 2048, 0),
+                                            (3, 2047, 2), (3, 2045, None)],
+                         ids=["w2-even-root", "w2-ragged-all", "w3-ragged-root",
+                              "w3-ragged-to-2", "w3-ragged-all"])
+def test_gloo_output_loop_equals_single_rank(oracle_port, tmp_path, world, ncol, dst):
+    """SURVEY 8e correctness test of the bench/driver output loop: ragged shards
+    (shard_range), double-buffered asynchronous gathers with buffer reuse, to
+    one rank or to all; every output step rebuilt on the receiver equals the
+    single-rank run bit for bit."""
+    from golden_io import load
+    port = _free_port()
     out_path = str(tmp_path / "gathered.npy")
-    mp.start_processes(_worker, args=(world, port, out_path, dst), nprocs=world,
+    mp.start_processes(_worker, args=(world, port, out_path, ncol, dst), nprocs=world,
                        start_method="spawn")
     got = np.load(out_path)
     g = load("single_casenml_mixed.npz")
-    _, _, dg, _ = oracle_port.step(load_params(), tuple(g["options"]), g["zsoil"],
-                                   float(g["dt"]), int(g["yearlen"]), float(g["julian"]),
-                                   g["state0"], g["isnow0"], g["static_f"], g["static_i"],
-                                   g["forcing"])
-    idx = [L.DIAG_FULL.index(d) if d != "T2M" else L.DIAG_FULL.index("T2MV") for d in L.DIAG_OUT]
-    full = dg[idx]
-    n = full.shape[1]
-    per = n // world
-    rebuilt = np.concatenate([got[r * L.NDIAG_OUT:(r + 1) * L.NDIAG_OUT] for r in range(world)],
-                             axis=1)
-    assert rebuilt.shape == full.shape and per * world == n
-    assert np.array_equal(rebuilt, full) or np.array_equal(
-        np.nan_to_num(rebuilt, nan=1e30), np.nan_to_num(full, nan=1e30))
+    full = _oracle_steps(g, slice(0, ncol), NSTEPS)
+    want = np.stack([full[k] for k in range(NSTEPS) if (k + 1) % OUT_EVERY == 0])
+    assert got.shape == want.shape == (NSTEPS // OUT_EVERY, L.NDIAG_OUT, ncol)
+    assert np.array_equal(got.view(np.int32), want.view(np.int32))
 
 
 def _gpu_worker(rank, world, port, out_path):
