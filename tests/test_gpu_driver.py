@@ -9,6 +9,7 @@ import numpy as np
 import pytest
 import torch
 
+import noahmp_pkg  # noqa: F401  (spawned ranks re-import this module)
 from golden_io import bit_equal, load
 from noahmp_amd import cases, config, driver, layout as L
 
