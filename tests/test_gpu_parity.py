@@ -478,7 +478,9 @@ def test_sflx_columns_rejects_what_the_kernel_cannot_honour(engines):
 ])
 def test_full_size_sample_vs_oracle(engines, oracle_port, kind, ncol, opt_veg, precision):
     """BASELINE sizes: two steps of every column on the GPU, then a seeded
-    sample of 2,048 columns re-run through the C restatement (bit-exact to the
+    sample of 2,048 columns re-run through the C restatement (JULIAN is a real
+    argument of noahmp_sflx and of nmp_step, fp32 in every precision, so the
+    oracle gets the same fp32 value; the restatement is bit-exact to the
     reference in fp32 on every fixture): bit-identical in fp32, |d| <= 1e-9
     (1 + |x|) in fp64.  Column independence makes the sample a full check of
     those columns at full launch size (grid, stream ranges, ragged tail)."""
@@ -505,7 +507,7 @@ def test_full_size_sample_vs_oracle(engines, oracle_port, kind, ncol, opt_veg, p
     for s in range(2):
         st, isn, dg, status = oracle_port.step(
             load_params(), tuple(opts[k] for k in L.OPTION_NAMES), cases.CASE_NML_ZSOIL, dt, 366,
-            jul[s], st, isn, cols.static_f[:, idx], cols.static_i[:, idx], F[s][:, idx],
+            float(np.float32(jul[s])), st, isn, cols.static_f[:, idx], cols.static_i[:, idx], F[s][:, idx],
             precision=precision)
     got = cs.state.cpu().numpy()[:, idx]
     gd = diag.cpu().numpy()[:, idx]
