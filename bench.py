@@ -95,6 +95,10 @@ def parse():
                     help="column order on the GPU (columns are independent: any permutation "
                          "gives bit-identical per-column results); 'lon' groups columns of "
                          "similar solar time into the same wave, like a real lat-lon grid")
+    ap.add_argument("--rebin-tile", type=int, default=0,
+                    help="column re-binning (nmp_rebin): sort columns by the previous step's "
+                         "vege_flux trip count within tiles of this many columns (0 = off)")
+    ap.add_argument("--rebin-every", type=int, default=1, help="re-sort every this many steps")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-steps", type=int, default=32)
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic.json"),
@@ -155,7 +159,7 @@ def main():
         F[s].copy_(torch.from_numpy(cases.forcing_step(
             cols, julian0 + s * a.dt / 86400.0, yearlen, s, seed=seed)))
     gather_dst = 0 if a.gather == "root" else None
-    ranges = StreamShards(eng, cs, a.streams)
+    ranges = StreamShards(eng, cs, a.streams, rebin_tile=a.rebin_tile, rebin_every=a.rebin_every)
     comm = torch.cuda.Stream(dev) if use_dist else None
     if use_dist:
         # after the range streams exist: RCCL's communicator creates streams of
@@ -252,6 +256,8 @@ def main():
                        "ncol_total": world * n, "dt_s": a.dt, "out_every": a.out_every,
                        "math": a.math, "column_order": a.order,
                        "streams": len(ranges.ranges),
+                       "rebin": {"tile": a.rebin_tile, "every": a.rebin_every}
+                       if a.rebin_tile else None,
                        "parallelism": f"column-shard x{world}",
                        "gather": a.gather if use_dist else None},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",

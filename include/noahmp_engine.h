@@ -245,6 +245,24 @@ int nmp_step(nmp_engine* eng, int64_t ncol, int64_t ld, const float zsoil[4], fl
              const int32_t* static_i, const void* forcing, void* diag, int diag_level,
              int32_t* col_status, void* stream);
 
+/* Column re-binning (no reference counterpart: a scheduling aid for the wave's
+ * slowest-lane cost).  nmp_step_binned is nmp_step where lane i
+ * steps column order[i] (order: a permutation of 0..ncol-1, device int32, or
+ * NULL for the identity) and, when cost is non-NULL, each column's loop-cost
+ * key (its vege_flux Newton trip count this step, 0 without a canopy; one byte
+ * per column, indexed by column) is written.  Every column reads and writes
+ * only its own index in every array, so results are bit-identical for any
+ * order.  nmp_rebin builds an order from such keys: within each tile of `tile`
+ * consecutive columns (a multiple of 64), the columns sorted by key, so that
+ * the waves of the next step hold columns of similar cost. */
+int nmp_step_binned(nmp_engine* eng, int64_t ncol, int64_t ld, const float zsoil[4], float dt,
+                    float julian, int32_t yearlen, void* state, int32_t* isnow,
+                    const void* static_f, const int32_t* static_i, const void* forcing, void* diag,
+                    int diag_level, int32_t* col_status, const int32_t* order, uint8_t* cost,
+                    void* stream);
+int nmp_rebin(nmp_engine* eng, int64_t ncol, const uint8_t* cost, int32_t* order, int32_t tile,
+              void* stream);
+
 /* Same step, many times: nsteps steps (one launch each, enqueued on stream)
  * whose forcing slices are forcing + (s % forcing_period)*forcing_stride
  * (elements, real type; forcing_period 0 = nsteps distinct slices), julian

@@ -50,7 +50,7 @@ template <class T>
 void fill_args(nmp::KArgs<T>& a, const nmp_engine* e, int64_t ncol, int64_t ld,
                const float zsoil[4], float dt, float julian, int32_t yearlen, void* state,
                int32_t* isnow, const void* sf, const int32_t* si, const void* fc, void* diag,
-               int diag_level, int32_t* status) {
+               int diag_level, int32_t* status, const int32_t* order, uint8_t* cost) {
   a.ncol = ncol;
   a.ld = ld;
   for (int k = 0; k < 4; ++k) a.zsoil[k] = zsoil[k];
@@ -72,23 +72,25 @@ void fill_args(nmp::KArgs<T>& a, const nmp_engine* e, int64_t ncol, int64_t ld,
   a.forcing = static_cast<const T*>(fc);
   a.diag = static_cast<T*>(diag);
   a.status = status;
+  a.order = order;
+  a.cost = cost;
 }
 
 int launch(const nmp_engine* e, int64_t ncol, int64_t ld, const float zsoil[4], float dt,
            float julian, int32_t yearlen, void* state, int32_t* isnow, const void* sf,
            const int32_t* si, const void* fc, void* diag, int diag_level, int32_t* status,
-           hipStream_t stream) {
+           hipStream_t stream, const int32_t* order = nullptr, uint8_t* cost = nullptr) {
   hipError_t err;
   if (e->precision == 4) {
     nmp::KArgs<float> a;
     fill_args(a, e, ncol, ld, zsoil, dt, julian, yearlen, state, isnow, sf, si, fc, diag,
-              diag_level, status);
+              diag_level, status, order, cost);
     err = (e->math == 0) ? nmp::launch_sflx<float, true>(e->dparams, a, stream)
                          : nmp::launch_sflx<float, false>(e->dparams, a, stream);
   } else {
     nmp::KArgs<double> a;
     fill_args(a, e, ncol, ld, zsoil, dt, julian, yearlen, state, isnow, sf, si, fc, diag,
-              diag_level, status);
+              diag_level, status, order, cost);
     err = nmp::launch_sflx<double, false>(e->dparams, a, stream);
   }
   return err == hipSuccess ? NMP_OK : NMP_E_DEVICE;
@@ -190,6 +192,34 @@ int nmp_step(nmp_engine* eng, int64_t ncol, int64_t ld, const float zsoil[4], fl
   if (rc != NMP_OK) return rc;
   return launch(eng, ncol, ld, zsoil, dt, julian, yearlen, state, isnow, static_f, static_i,
                 forcing, diag, diag_level, col_status, static_cast<hipStream_t>(stream));
+}
+
+int nmp_step_binned(nmp_engine* eng, int64_t ncol, int64_t ld, const float zsoil[4], float dt,
+                    float julian, int32_t yearlen, void* state, int32_t* isnow,
+                    const void* static_f, const int32_t* static_i, const void* forcing, void* diag,
+                    int diag_level, int32_t* col_status, const int32_t* order, uint8_t* cost,
+                    void* stream) {
+  if (!eng || ncol < 0) return NMP_E_ARG;
+  if (ncol == 0) return NMP_OK;
+  if (ncol > INT32_MAX && order) return NMP_E_ARG;  // order holds int32 column indices
+  int rc = check_common(eng, ncol, ld, zsoil, dt, yearlen, state, isnow, static_f, static_i,
+                        forcing, diag, diag_level, col_status);
+  if (rc != NMP_OK) return rc;
+  return launch(eng, ncol, ld, zsoil, dt, julian, yearlen, state, isnow, static_f, static_i,
+                forcing, diag, diag_level, col_status, static_cast<hipStream_t>(stream), order,
+                cost);
+}
+
+int nmp_rebin(nmp_engine* eng, int64_t ncol, const uint8_t* cost, int32_t* order, int32_t tile,
+              void* stream) {
+  if (!eng || ncol < 0 || !cost || !order || ncol > INT32_MAX) return NMP_E_ARG;
+  if (tile < 64 || tile > (1 << 20) || tile % 64 != 0) return NMP_E_ARG;
+  if (ncol == 0) return NMP_OK;
+  if (ensure_device(eng->device) != NMP_OK) return NMP_E_DEVICE;
+  return nmp::launch_rebin(cost, order, ncol, tile, static_cast<hipStream_t>(stream)) ==
+                 hipSuccess
+             ? NMP_OK
+             : NMP_E_DEVICE;
 }
 
 int nmp_run(nmp_engine* eng, int64_t ncol, int64_t ld, const float zsoil[4], float dt,

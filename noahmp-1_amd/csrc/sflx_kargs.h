@@ -28,9 +28,17 @@ struct KArgs {
   const T* forcing;
   T* diag;
   int32_t* status;
+  // column re-binning (nmp_step_binned): lane i steps column order[i] when
+  // order is set; cost (if set) receives each column's loop-cost key
+  const int32_t* order;
+  uint8_t* cost;
 };
 
 template <class T, bool R>
 hipError_t launch_sflx(const DevParams* dparams, const KArgs<T>& a, hipStream_t stream);
+
+// csrc/rebin.hip: per-tile counting sort of the columns by cost key
+hipError_t launch_rebin(const uint8_t* cost, int32_t* order, int64_t ncol, int tile,
+                        hipStream_t stream);
 
 }  // namespace nmp

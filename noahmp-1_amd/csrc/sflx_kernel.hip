@@ -880,6 +880,7 @@ struct Sink {
   const int32_t* si;  // static_i + column
   const T* fc;        // forcing + column
   int32_t* isnow;     // isnow + column
+  uint8_t* cost;      // cost key + column (re-binning), or NULL
   // late loads: fields first needed deep in the step are read there, not at
   // kernel entry, so they do not hold registers through the energy phase
   DEV T ls(int f) const { return st[f * ld]; }
@@ -907,6 +908,10 @@ struct Sink {
   }
   DEV void s(int f, T v) const { st[f * ld] = v; }
   DEV void isn(int v) const { *isnow = v; }
+  // re-binning key: the vege_flux Newton trip count of this step (0 = no canopy)
+  DEV void trips(int n) const {
+    if (cost) *cost = (uint8_t)n;
+  }
 };
 
 // Optional per-phase timing (build with -DNMP_PHASE_TIMING; tools only):
@@ -1276,6 +1281,7 @@ DEV void sflx_column(const DevParams& P, const KArgs<T>& A, Col<T>& c, const Sin
   NMP_PHASE(4);
   // ---- vege_flux: func.f90:2465-2964 ----
   T tgv = L(0.0), cmv = L(0.0);
+  int vtrips = 0;
   if (veg && fveg > L(0.0)) {
     tgv = c.tg;
     cmv = c.cm;
@@ -1309,6 +1315,7 @@ DEV void sflx_column(const DevParams& P, const KArgs<T>& A, Col<T>& c, const Sin
                      : Sfc1Logs<T, R>{};
 #pragma unroll 1
     for (int iter = 1; iter <= 20; ++iter) {
+      vtrips = iter;
       if (o.sfc == 1)
         sfcdif1<T, R>(iter, c.sfctmp, rhoair, h, qair, zlvl, zpd, lgv, z0h, ur, mpe, moz, mozsgn,
                       fm, fh, fm2, fh2, cmv, chv, fv);
@@ -1423,6 +1430,7 @@ DEV void sflx_column(const DevParams& P, const KArgs<T>& A, Col<T>& c, const Sin
     chleaf = cvh;
     chuc = L(1.0) / rahg;
   }
+  out.trips(vtrips);
 
   NMP_PHASE(5);
   // ---- bare_flux: func.f90:2967-3257 ----
@@ -2748,8 +2756,11 @@ void sflx_step_kernel(const DevParams* __restrict__ gparams,
   }
   if constexpr (sizeof(T) == 4 && R) stage_math_tables();
   __syncthreads();
-  const int64_t c0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (c0 >= a.ncol) return;
+  const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= a.ncol) return;
+  // re-binned launch: this lane steps column order[gid] (a permutation of the
+  // columns; every column is independent, so results do not depend on it)
+  const int64_t c0 = a.order ? (int64_t)a.order[gid] : gid;
   const int64_t ld = a.ld;
   Col<T> c;
   const T* st = a.state + c0;
@@ -2791,7 +2802,7 @@ void sflx_step_kernel(const DevParams* __restrict__ gparams,
   c.status = 0;
 
   const Sink<T> out{a.diag ? a.diag + c0 : nullptr, a.state + c0, ld, a.diag_level, sf, si, fc,
-                    a.isnow + c0};
+                    a.isnow + c0, a.cost ? a.cost + c0 : nullptr};
   sflx_column<T, R>(sp, a, c, out);
 
   if (c.status != 0) a.status[c0] |= c.status;

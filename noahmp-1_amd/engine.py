@@ -112,12 +112,18 @@ class Engine:
 
     def step(self, cs: ColumnState, forcing: torch.Tensor, zsoil, dt: float, julian: float,
              yearlen: int, diag: torch.Tensor | None = None, diag_level: int = L.DIAG_NONE,
-             stream=None, cols: tuple[int, int] | None = None):
+             stream=None, cols: tuple[int, int] | None = None, order: torch.Tensor | None = None,
+             cost: torch.Tensor | None = None):
         """One noahmp_sflx step for every column (enqueued on `stream`).
 
         cols=(lo, hi) steps only columns lo..hi-1, in place (pointer offsets with
         ld = cs.ncol; forcing and diag are indexed by the same columns), so
-        column ranges can be stepped on different streams."""
+        column ranges can be stepped on different streams.
+
+        order / cost (re-binning, nmp_step_binned): int32 / uint8 tensors of
+        cs.ncol entries; the range's slice of `order` must hold a permutation of
+        0..hi-lo-1 (indices relative to lo), `cost` receives each column's
+        vege_flux trip count."""
         self._check_cols(cs, forcing)
         n = cs.ncol
         lo, hi = (0, n) if cols is None else (int(cols[0]), int(cols[1]))
@@ -131,11 +137,34 @@ class Engine:
             assert diag.device.type == "cuda" and diag.device.index == self.device, diag.device
         zs = (C.c_float * 4)(*[float(z) for z in zsoil])
         s = stream if stream is not None else torch.cuda.current_stream(self.device)
+        if order is not None or cost is not None:
+            for t, dt_ in ((order, torch.int32), (cost, torch.uint8)):
+                if t is not None:
+                    assert t.shape == (n,) and t.dtype == dt_ and t.is_contiguous()
+                    assert t.device.type == "cuda" and t.device.index == self.device
+            _lib.check(self._lib.nmp_step_binned(
+                self._h, hi - lo, n, zs, float(dt), float(julian), int(yearlen),
+                _ptr(cs.state, lo), _ptr(cs.isnow, lo), _ptr(cs.static_f, lo),
+                _ptr(cs.static_i, lo), _ptr(forcing, lo), _ptr(diag, lo), int(diag_level),
+                _ptr(cs.status, lo), _ptr(order, lo), _ptr(cost, lo),
+                C.c_void_p(s.cuda_stream)), "nmp_step_binned")
+            return
         _lib.check(self._lib.nmp_step(self._h, hi - lo, n, zs, float(dt), float(julian),
                                       int(yearlen), _ptr(cs.state, lo), _ptr(cs.isnow, lo),
                                       _ptr(cs.static_f, lo), _ptr(cs.static_i, lo),
                                       _ptr(forcing, lo), _ptr(diag, lo), int(diag_level),
                                       _ptr(cs.status, lo), C.c_void_p(s.cuda_stream)), "nmp_step")
+
+    def rebin(self, cost: torch.Tensor, order: torch.Tensor, tile: int, stream=None,
+              cols: tuple[int, int] | None = None):
+        """nmp_rebin: order[lo:hi] <- the columns lo..hi-1 sorted by cost within
+        tiles of `tile` columns (indices relative to lo)."""
+        n = int(cost.shape[0])
+        lo, hi = (0, n) if cols is None else (int(cols[0]), int(cols[1]))
+        assert cost.dtype == torch.uint8 and order.dtype == torch.int32 and order.shape == (n,)
+        s = stream if stream is not None else torch.cuda.current_stream(self.device)
+        _lib.check(self._lib.nmp_rebin(self._h, hi - lo, _ptr(cost, lo), _ptr(order, lo),
+                                       int(tile), C.c_void_p(s.cuda_stream)), "nmp_rebin")
 
     def sflx_columns(self, rec: np.ndarray) -> np.ndarray:
         """noahmp_sflx with the reference calling sequence on host records
@@ -193,13 +222,26 @@ class StreamShards:
     `join()` makes a stream wait for every range, and is needed before the
     caller reads state or diagnostics."""
 
-    def __init__(self, engine: Engine, cs: ColumnState, nshards: int = 2, device=None):
+    def __init__(self, engine: Engine, cs: ColumnState, nshards: int = 2, device=None,
+                 rebin_tile: int = 0, rebin_every: int = 1):
+        """rebin_tile > 0 turns on column re-binning (nmp_step_binned /
+        nmp_rebin): every `rebin_every` steps each range re-sorts its columns
+        within tiles of rebin_tile columns by the trip counts the previous step
+        recorded, and the next launches step them in that order."""
         n = cs.ncol
         nshards = max(1, min(int(nshards), max(n, 1)))
         self.engine, self.cs = engine, cs
         dev = torch.device("cuda", engine.device) if device is None else torch.device(device)
         self.streams = [torch.cuda.Stream(dev) for _ in range(nshards)]
         self.ranges = [(n * i // nshards, n * (i + 1) // nshards) for i in range(nshards)]
+        self.rebin_tile, self.rebin_every, self.nstep = int(rebin_tile), max(1, int(rebin_every)), 0
+        self.order = self.cost = None
+        if self.rebin_tile:
+            # identity order to start with, relative to each range's first column
+            self.order = torch.cat([torch.arange(hi - lo, dtype=torch.int32)
+                                    for lo, hi in self.ranges]).to(dev) if n else \
+                torch.zeros(0, dtype=torch.int32, device=dev)
+            self.cost = torch.zeros(n, dtype=torch.uint8, device=dev)
 
     def step(self, forcing: torch.Tensor, zsoil, dt: float, julian: float, yearlen: int,
              diag: torch.Tensor | None = None, diag_level: int = L.DIAG_NONE, events=None,
@@ -220,10 +262,14 @@ class StreamShards:
                     diag.record_stream(st)
             if events is not None:
                 events[i][0].record(st)
+            if self.rebin_tile and self.nstep > 0 and self.nstep % self.rebin_every == 0:
+                self.engine.rebin(self.cost, self.order, self.rebin_tile, stream=st, cols=rng)
             self.engine.step(self.cs, forcing, zsoil, dt, julian, yearlen, diag, diag_level,
-                             stream=st, cols=None if len(self.streams) == 1 else rng)
+                             stream=st, cols=None if len(self.streams) == 1 else rng,
+                             order=self.order, cost=self.cost)
             if events is not None:
                 events[i][1].record(st)
+        self.nstep += 1
 
     def join(self, stream: torch.cuda.Stream | None = None):
         """Make `stream` (default: the current stream) wait for every range."""

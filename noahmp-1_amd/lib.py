@@ -92,6 +92,9 @@ def load(build_if_missing: bool = False):
     lib.nmp_set_math.argtypes = [vp, C.c_int]
     lib.nmp_step.argtypes = [vp, C.c_int64, C.c_int64, f32p, C.c_float, C.c_float, C.c_int32,
                              vp, vp, vp, vp, vp, vp, C.c_int, vp, vp]
+    lib.nmp_step_binned.argtypes = [vp, C.c_int64, C.c_int64, f32p, C.c_float, C.c_float,
+                                     C.c_int32, vp, vp, vp, vp, vp, vp, C.c_int, vp, vp, vp, vp]
+    lib.nmp_rebin.argtypes = [vp, C.c_int64, vp, vp, C.c_int32, vp]
     lib.nmp_run.argtypes = [vp, C.c_int64, C.c_int64, f32p, C.c_float, C.c_float, C.c_int32,
                             C.c_int32, vp, vp, vp, vp, vp, C.c_int64, C.c_int32, vp, C.c_int, vp,
                             vp]
@@ -115,7 +118,8 @@ def load(build_if_missing: bool = False):
     return lib
 
 
-EXPORTED_SYMBOLS = ["nmp_read_tables", "nmp_init", "nmp_step", "nmp_run", "nmp_run_out",
+EXPORTED_SYMBOLS = ["nmp_read_tables", "nmp_init", "nmp_step", "nmp_step_binned", "nmp_rebin",
+                    "nmp_run", "nmp_run_out",
                     "nmp_state_from_aos", "nmp_sflx_columns", "nmp_sflx_column",
                     "nmp_engine_info", "nmp_set_math", "nmp_finalize", "nmp_strerror",
                     "nmp_abi_version", "nmp_build_hash"]

@@ -356,6 +356,70 @@ def test_stream_shards_equal_single_launch(engines, nshards):
         assert torch.equal(bits(x), bits(y))
 
 
+@pytest.mark.parametrize("tile,every", [(1024, 1), (4096, 2)])
+def test_rebinned_steps_equal_plain_steps(engines, tile, every):
+    """Column re-binning (StreamShards rebin_tile / nmp_step_binned + nmp_rebin)
+    only changes which lane steps which column: state, ISNOW, status and every
+    output step's diagnostics are bit-identical to plain launches over 6 steps;
+    200,003 columns = ragged ranges and a ragged last tile."""
+    from noahmp_amd.engine import ColumnState, StreamShards
+    from noahmp_amd.params import Params
+    n = 200_003
+    eng = engines([L.CASE_NML_OPTIONS[k] for k in L.OPTION_NAMES])
+    cols = cases.make_columns(n, "mixed", Params.builtin().as_dict(), seed=7, julian=200.0)
+    F = [torch.as_tensor(cases.forcing_step(cols, 200.0 + s / 48.0, 365, s, seed=7), device=DEV)
+         for s in range(6)]
+    a = ColumnState.from_host(cols, DEV)
+    b = ColumnState.from_host(cols, DEV)
+    sa = StreamShards(eng, a, 2, rebin_tile=tile, rebin_every=every)
+    sb = StreamShards(eng, b, 2)
+    da = [torch.zeros((L.NDIAG_OUT, n), device=DEV) for _ in range(3)]
+    db = [torch.zeros((L.NDIAG_OUT, n), device=DEV) for _ in range(3)]
+    for s in range(6):
+        out = s % 2 == 1
+        lvl = L.DIAG_OUT_LEVEL if out else L.DIAG_NONE
+        for sh, d in ((sa, da), (sb, db)):
+            sh.step(F[s], cases.CASE_NML_ZSOIL, 1800.0, 200.0 + s / 48.0, 365,
+                    d[s // 2] if out else None, lvl)
+    sa.join()
+    sb.join()
+    torch.cuda.synchronize()
+    bits = lambda t: t.view(torch.int32)
+    assert torch.equal(bits(a.state), bits(b.state)) and torch.equal(a.isnow, b.isnow)
+    assert torch.equal(a.status, b.status)
+    for x, y in zip(da, db):
+        assert torch.equal(bits(x), bits(y))
+    # the order really was permuted: each range's order is a permutation of its columns
+    # and not the identity
+    for lo, hi in sa.ranges:
+        o = sa.order[lo:hi].cpu().numpy()
+        assert np.array_equal(np.sort(o), np.arange(hi - lo))
+        assert (o != np.arange(hi - lo)).any()
+
+
+def test_cost_key_is_the_reference_trip_count(engines, oracle_port):
+    """The re-binning key the kernel records (nmp_step_binned cost) is the
+    vege_flux Newton trip count, equal to the oracle's count for every column
+    of the mixed fixture (0 where no canopy flux is computed)."""
+    from noahmp_amd.engine import ColumnState
+    g = load("single_casenml_mixed.npz")
+    eng = engines(g["options"])
+    cols = cases.ColumnSet(g["static_f"], g["static_i"], g["state0"], g["isnow0"], *([None] * 7))
+    cs = ColumnState.from_host(cols, DEV)
+    n = cs.ncol
+    cost = torch.full((n,), 255, dtype=torch.uint8, device=DEV)
+    order = torch.as_tensor(np.random.default_rng(0).permutation(n).astype(np.int32), device=DEV)
+    f = torch.as_tensor(g["forcing"], device=DEV).contiguous()
+    eng.step(cs, f, g["zsoil"], float(g["dt"]), float(g["julian"]), int(g["yearlen"]),
+             order=order, cost=cost)
+    torch.cuda.synchronize()
+    *_, it = oracle_port.step_stats(load_params(), tuple(g["options"]), g["zsoil"], float(g["dt"]),
+                                    int(g["yearlen"]), float(g["julian"]), g["state0"],
+                                    g["isnow0"], g["static_f"], g["static_i"], g["forcing"])
+    assert np.array_equal(cost.cpu().numpy(), it[:, 0].astype(np.uint8))
+    assert bit_equal(cs.state.cpu().numpy(), g["state1"]).all()  # a random order, same bits
+
+
 def test_diag_levels_consistent(engines):
     """DIAG_OUT fields are the DIAG_FULL values (T2M = the fveg blend of T2MV/T2MB)."""
     from noahmp_amd.engine import ColumnState
