@@ -2756,7 +2756,16 @@ void sflx_step_kernel(const DevParams* __restrict__ gparams,
   }
   if constexpr (sizeof(T) == 4 && R) stage_math_tables();
   __syncthreads();
-  const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  int64_t blk = blockIdx.x;
+  if (a.order) {
+    // re-binned launch: workgroups are dealt round-robin over the 8 XCDs
+    // (b and b+8 share one), so map consecutive logical blocks -- one rebin
+    // tile's -- onto one XCD: its gathered loads and scattered stores then meet
+    // in that XCD's L2 instead of leaving partial lines in eight
+    const int64_t per = (int64_t)gridDim.x / 8;
+    if (blk < per * 8) blk = (blk % 8) * per + blk / 8;
+  }
+  const int64_t gid = blk * blockDim.x + threadIdx.x;
   if (gid >= a.ncol) return;
   // re-binned launch: this lane steps column order[gid] (a permutation of the
   // columns; every column is independent, so results do not depend on it)
