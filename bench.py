@@ -99,6 +99,9 @@ def parse():
                     help="column re-binning (nmp_rebin): sort columns by the previous step's "
                          "vege_flux trip count within tiles of this many columns (0 = off)")
     ap.add_argument("--rebin-every", type=int, default=1, help="re-sort every this many steps")
+    ap.add_argument("--cpw", type=int, default=0,
+                    help="columns per wave (8..64, multiple of 8); 0 = the engine's automatic "
+                         "choice (fewer per wave when the column set cannot fill the chip)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-steps", type=int, default=32)
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic.json"),
@@ -150,6 +153,7 @@ def main():
     dev = torch.device("cuda", local)
     dtype = torch.float32 if a.precision == 4 else torch.float64
     eng = Engine(P, opt_dict, device=local, precision=a.precision, math=a.math)
+    eng.set_cols_per_wave(a.cpw)
     from noahmp_amd import lib as _nlib
     build_hash = _nlib.load().nmp_build_hash().decode()  # lib.load refuses a stale library
     cs = ColumnState.from_host(cols, dev, dtype)
@@ -255,7 +259,7 @@ def main():
                        "ncol_per_gpu": n,
                        "ncol_total": world * n, "dt_s": a.dt, "out_every": a.out_every,
                        "math": a.math, "column_order": a.order,
-                       "streams": len(ranges.ranges),
+                       "streams": len(ranges.ranges), "cols_per_wave": a.cpw or "auto",
                        "rebin": {"tile": a.rebin_tile, "every": a.rebin_every}
                        if a.rebin_tile else None,
                        "parallelism": f"column-shard x{world}",

@@ -316,6 +316,13 @@ int nmp_sflx_column(nmp_engine* eng, nmp_sflx_args* col);
  * always use ocml double.  Default can also be set with NMP_MATH=fast. */
 int nmp_set_math(nmp_engine* eng, int mode);
 
+/* Columns stepped per 64-lane wave: 8..64 (multiple of 8), or 0 (default) to
+ * choose per launch: a column set too small to fill every wave slot of the
+ * chip is spread over more, partly filled waves (the step is latency-bound,
+ * so a SIMD gains from interleaving more waves even at fewer lanes each).
+ * Results do not depend on it. */
+int nmp_set_cols_per_wave(nmp_engine* eng, int cpw);
+
 int nmp_engine_info(const nmp_engine* eng, int* device, int* precision, nmp_options* opts);
 void nmp_finalize(nmp_engine* eng);
 const char* nmp_strerror(int code);

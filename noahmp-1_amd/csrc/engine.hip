@@ -23,6 +23,8 @@ struct nmp_engine {
   int device;
   int precision;
   int math;  // 0 = reference-rounded transcendentals (parity), 1 = fast (fp32 only)
+  int cpw;   // columns per wave: 8..64, or 0 = chosen per launch from ncol
+  int simds; // SIMDs on the device (CUs x 4)
   nmp_options opts;
   nmp::DevParams* dparams;
 };
@@ -44,6 +46,21 @@ int ensure_device(int dev) {
   if (hipGetDevice(&cur) != hipSuccess) return NMP_E_DEVICE;
   if (cur != dev && hipSetDevice(dev) != hipSuccess) return NMP_E_DEVICE;
   return NMP_OK;
+}
+
+// Columns per wave.  A launch whose columns give fewer waves than the chip
+// holds at the kernel's occupancy (4 waves/SIMD fp32, 2 fp64) leaves the
+// latency-bound step with nothing to overlap: one wave per SIMD at 65,536
+// columns (config #2).  Spreading the columns over more, partly filled waves
+// lets the SIMD interleave them; the kernel is latency- not issue-bound, so
+// the idle lanes cost little.  Rule: the smallest multiple of 8 (>= 8) that
+// still fills every wave slot, capped at 64.
+int cols_per_wave(const nmp_engine* e, int64_t ncol) {
+  if (e->cpw) return e->cpw;
+  const int64_t slots = (int64_t)e->simds * (e->precision == 4 ? 4 : 2);
+  int64_t c = (ncol + slots - 1) / slots;
+  c = (c + 7) / 8 * 8;
+  return (int)(c < 8 ? 8 : c > 64 ? 64 : c);
 }
 
 template <class T>
@@ -74,6 +91,7 @@ void fill_args(nmp::KArgs<T>& a, const nmp_engine* e, int64_t ncol, int64_t ld,
   a.status = status;
   a.order = order;
   a.cost = cost;
+  a.cpw = cols_per_wave(e, ncol);
 }
 
 int launch(const nmp_engine* e, int64_t ncol, int64_t ld, const float zsoil[4], float dt,
@@ -161,6 +179,12 @@ int nmp_init(const nmp_params* params, const nmp_options* opts, int device, int 
   e->precision = precision;
   const char* m = std::getenv("NMP_MATH");
   e->math = (m && std::strcmp(m, "fast") == 0) ? 1 : 0;
+  e->cpw = 0;
+  int ncu = 0;
+  if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess ||
+      ncu <= 0)
+    ncu = 256;
+  e->simds = 4 * ncu;
   e->opts = *opts;
   e->dparams = d;
   *out = e;
@@ -170,6 +194,12 @@ int nmp_init(const nmp_params* params, const nmp_options* opts, int device, int 
 int nmp_set_math(nmp_engine* eng, int mode) {
   if (!eng || mode < 0 || mode > 1) return NMP_E_ARG;
   eng->math = mode;
+  return NMP_OK;
+}
+
+int nmp_set_cols_per_wave(nmp_engine* eng, int cpw) {
+  if (!eng || cpw < 0 || cpw > 64 || cpw % 8 != 0) return NMP_E_ARG;
+  eng->cpw = cpw;
   return NMP_OK;
 }
 

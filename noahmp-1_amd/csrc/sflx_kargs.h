@@ -6,6 +6,15 @@
 
 #include "dev_params.h"
 
+// workgroup size of the step kernel (256: DESIGN.md "Occupancy")
+#ifndef NMP_BLOCK
+#define NMP_BLOCK 256
+#endif
+// per-lane LDS slots for the LDS-resident layer work arrays (LArr)
+#ifndef NMP_LDS_SLOTS
+#define NMP_LDS_SLOTS 28
+#endif
+
 namespace nmp {
 
 struct Opt {
@@ -32,6 +41,9 @@ struct KArgs {
   // order is set; cost (if set) receives each column's loop-cost key
   const int32_t* order;
   uint8_t* cost;
+  // columns stepped per 64-lane wave (8..64, a multiple of 8): below 64 the
+  // launch spreads a small column set over more waves (small-N latency hiding)
+  int cpw;
 };
 
 template <class T, bool R>

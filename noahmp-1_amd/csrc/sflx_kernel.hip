@@ -34,12 +34,29 @@ struct Col {
   // forcing
   T sfctmp, sfcprs, psfc, uu, vv, q2, soldn, lwdn, prcp, cosz, co2air, o2air;
   // prognostic state
+#ifdef NMP_LDS_STATE
+  LArr<T, 7, 0> stc;
+  LArr<T, 7, 7> zsnso;
+  LArr<T, 3, 14> snice;
+  LArr<T, 3, 17> snliq;
+  LArr<T, 4, 20> sh2o;
+  LArr<T, 4, 24> smc;
+#else
   T stc[7], zsnso[7], snice[3], snliq[3], sh2o[4], smc[4];
+#endif
   T tv, tg, tah, eah, fwet, canliq, canice, qsfc, snowh, sneqv, sneqvo, albold, tauss, qsnow;
   T zwt, wa, wt, wslake, lai, sai, lfmass, rtmass, stmass, wood, stblcp, fastcp, cm, ch;
   int isnow;
   // per-step layer work arrays
+#ifdef NMP_LDS_WORK
+  LArr<T, 7, 0> dz;
+  LArr<T, 7, 7> df;
+  LArr<T, 7, 14> hcpct;
+  LArr<T, 7, 21> fact;
+  T ficeold[3], sice[4], btrani[4];
+#else
   T dz[7], ficeold[3], sice[4], btrani[4], df[7], hcpct[7], fact[7];
+#endif
   int imelt[7];
   int status;
 };
@@ -2740,9 +2757,6 @@ template <class T, bool R>
 #ifndef NMP_WAVES_PER_EU_F64
 #define NMP_WAVES_PER_EU_F64 2
 #endif
-#ifndef NMP_BLOCK
-#define NMP_BLOCK 256
-#endif
 __global__ __launch_bounds__(NMP_BLOCK)
 __attribute__((amdgpu_waves_per_eu(sizeof(T) == 4 ? NMP_WAVES_PER_EU : NMP_WAVES_PER_EU_F64)))
 void sflx_step_kernel(const DevParams* __restrict__ gparams,
@@ -2765,7 +2779,11 @@ void sflx_step_kernel(const DevParams* __restrict__ gparams,
     const int64_t per = (int64_t)gridDim.x / 8;
     if (blk < per * 8) blk = (blk % 8) * per + blk / 8;
   }
-  const int64_t gid = blk * blockDim.x + threadIdx.x;
+  // lane -> column: the first cpw lanes of each wave step consecutive columns
+  // (cpw = 64: gid = blk * 256 + tid, the plain coalesced map)
+  const int lane = threadIdx.x & 63;
+  if (lane >= a.cpw) return;
+  const int64_t gid = (blk * (NMP_BLOCK / 64) + (threadIdx.x >> 6)) * a.cpw + lane;
   if (gid >= a.ncol) return;
   // re-binned launch: this lane steps column order[gid] (a permutation of the
   // columns; every column is independent, so results do not depend on it)
@@ -2820,8 +2838,9 @@ void sflx_step_kernel(const DevParams* __restrict__ gparams,
 // launch wrapper (one instantiation per precision / math policy)
 template <class T, bool R>
 hipError_t launch_sflx(const DevParams* dparams, const KArgs<T>& a, hipStream_t stream) {
+  const int64_t cols_per_block = (int64_t)(NMP_BLOCK / 64) * a.cpw;
+  const int64_t grid = (a.ncol + cols_per_block - 1) / cols_per_block;
   const int block = NMP_BLOCK;
-  const int64_t grid = (a.ncol + block - 1) / block;
   if (grid == 0) return hipSuccess;
   hipLaunchKernelGGL((sflx_step_kernel<T, R>), dim3((unsigned)grid), dim3(block), 0, stream,
                      dparams, a);

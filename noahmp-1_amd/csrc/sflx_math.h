@@ -126,6 +126,28 @@ __device__ __forceinline__ void dset(T (&a)[N], int i, T v) {
   for (int k = 0; k < N; ++k)
     if (i == k) a[k] = v;
 }
+// LDS-resident per-lane arrays (NMP_LDS_WORK): element k of lane t lives at
+// pool[(SLOT + k) * NMP_BLOCK + t], i.e. [array][layer][lane] -- consecutive
+// lanes hit consecutive banks, a runtime layer index is one address add, and
+// the array holds no VGPRs across the step.  Each lane touches only its own
+// column, so no barrier is needed.
+template <class T>
+__device__ __forceinline__ T* lds_lane_pool() {
+  __shared__ T pool[NMP_LDS_SLOTS * NMP_BLOCK];
+  return pool + threadIdx.x;
+}
+template <class T, int N, int SLOT>
+struct LArr {
+  static_assert(SLOT + N <= NMP_LDS_SLOTS, "LDS slot pool too small");
+  __device__ __forceinline__ T& operator[](int k) const {
+    return lds_lane_pool<T>()[(SLOT + k) * NMP_BLOCK];
+  }
+};
+template <class T, int N, int S>
+__device__ __forceinline__ T dget(const LArr<T, N, S>& a, int i) { return a[i]; }
+template <class T, int N, int S>
+__device__ __forceinline__ void dset(const LArr<T, N, S>& a, int i, T v) { a[i] = v; }
+
 __device__ __forceinline__ float zget(const float (&a)[4], int i) {
   return i == 0 ? a[0] : i == 1 ? a[1] : i == 2 ? a[2] : a[3];
 }

@@ -82,6 +82,10 @@ class Engine:
             math = MATH_FAST if math == "fast" else MATH_REF
         self.set_math(math)
 
+    def set_cols_per_wave(self, cpw: int):
+        """nmp_set_cols_per_wave: 8..64 columns per wave, 0 = automatic."""
+        _lib.check(self._lib.nmp_set_cols_per_wave(self._h, int(cpw)), "nmp_set_cols_per_wave")
+
     def set_math(self, mode: int):
         _lib.check(self._lib.nmp_set_math(self._h, int(mode)), "nmp_set_math")
         self.math = int(mode)

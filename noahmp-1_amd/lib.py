@@ -90,6 +90,7 @@ def load(build_if_missing: bool = False):
     lib.nmp_init.argtypes = [C.POINTER(NmpParams), C.POINTER(NmpOptions), C.c_int, C.c_int,
                              C.POINTER(vp)]
     lib.nmp_set_math.argtypes = [vp, C.c_int]
+    lib.nmp_set_cols_per_wave.argtypes = [vp, C.c_int]
     lib.nmp_step.argtypes = [vp, C.c_int64, C.c_int64, f32p, C.c_float, C.c_float, C.c_int32,
                              vp, vp, vp, vp, vp, vp, C.c_int, vp, vp]
     lib.nmp_step_binned.argtypes = [vp, C.c_int64, C.c_int64, f32p, C.c_float, C.c_float,
@@ -121,7 +122,7 @@ def load(build_if_missing: bool = False):
 EXPORTED_SYMBOLS = ["nmp_read_tables", "nmp_init", "nmp_step", "nmp_step_binned", "nmp_rebin",
                     "nmp_run", "nmp_run_out",
                     "nmp_state_from_aos", "nmp_sflx_columns", "nmp_sflx_column",
-                    "nmp_engine_info", "nmp_set_math", "nmp_finalize", "nmp_strerror",
+                    "nmp_engine_info", "nmp_set_math", "nmp_set_cols_per_wave", "nmp_finalize", "nmp_strerror",
                     "nmp_abi_version", "nmp_build_hash"]
 
 

@@ -397,6 +397,47 @@ def test_rebinned_steps_equal_plain_steps(engines, tile, every):
         assert (o != np.arange(hi - lo)).any()
 
 
+@pytest.mark.parametrize("cpw", [8, 24, 40, 64])
+def test_cols_per_wave_bit_identical(engines, cpw):
+    """Columns per wave (nmp_set_cols_per_wave) only changes the lane -> column
+    map: every cpw gives the reference's bits on the mixed fixture, with a
+    ragged column count (2,047) so the last wave and block are partial."""
+    from noahmp_amd.params import Params
+    g = load("single_casenml_mixed.npz")
+    n = 2047
+    sub = {k: (v[..., :n] if isinstance(v, np.ndarray) and v.ndim >= 1 and
+               v.shape[-1] == g["isnow0"].shape[0] else v) for k, v in g.items()}
+    from noahmp_amd.engine import Engine
+    eng = Engine(Params.builtin(), dict(zip(L.OPTION_NAMES, g["options"].tolist())), device=0)
+    eng.set_cols_per_wave(cpw)
+    st, isn, dg, status = run_single(eng, sub)
+    eng.close()
+    ok = bit_equal(st, sub["state1"]).all(0) & bit_equal(dg, sub["diag"]).all(0) & \
+        (isn == sub["isnow1"])
+    assert ok.all(), (~ok).sum()
+
+
+def test_small_column_set_auto_cols_per_wave(engines):
+    """The automatic choice for a small set (65,536 fp64 columns: 32 per wave)
+    gives the same bits as full waves."""
+    from noahmp_amd.engine import ColumnState, Engine
+    from noahmp_amd.params import Params
+    n = 65536
+    cols = cases.make_columns(n, "mixed", Params.builtin().as_dict(), seed=9, julian=120.0)
+    f = torch.as_tensor(cases.forcing_step(cols, 120.0, 366, 0, seed=9), device=DEV).double()
+    out = []
+    for cpw in (0, 64):
+        eng = Engine(Params.builtin(), L.CASE_NML_OPTIONS, device=0, precision=8)
+        eng.set_cols_per_wave(cpw)
+        cs = ColumnState.from_host(cols, DEV, torch.float64)
+        d = torch.zeros((L.NDIAG_OUT, n), dtype=torch.float64, device=DEV)
+        eng.step(cs, f, cases.CASE_NML_ZSOIL, 1800.0, 120.0, 366, d, L.DIAG_OUT_LEVEL)
+        torch.cuda.synchronize()
+        out.append((cs.state.view(torch.int64).clone(), d.view(torch.int64).clone()))
+        eng.close()
+    assert torch.equal(out[0][0], out[1][0]) and torch.equal(out[0][1], out[1][1])
+
+
 def test_cost_key_is_the_reference_trip_count(engines, oracle_port):
     """The re-binning key the kernel records (nmp_step_binned cost) is the
     vege_flux Newton trip count, equal to the oracle's count for every column

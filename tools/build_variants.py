@@ -33,6 +33,8 @@ VARIANTS = {
     "en_w4": ("-DNMP_TRUNC_ENERGY",),
     "en_w5": ("-DNMP_TRUNC_ENERGY", "-DNMP_WAVES_PER_EU=5"),
     "en_w3": ("-DNMP_TRUNC_ENERGY", "-DNMP_WAVES_PER_EU=3"),
+    "en_w6": ("-DNMP_TRUNC_ENERGY", "-DNMP_WAVES_PER_EU=6"),
+    "en_w8": ("-DNMP_TRUNC_ENERGY", "-DNMP_WAVES_PER_EU=8"),
     "d2": ("-DNMP_WAVES_PER_EU_F64=2",),
     "s_maxilp": ("-mllvm", "-amdgpu-sched-strategy=max-ilp"),
     "s_memclause": ("-mllvm", "-amdgpu-sched-strategy=max-memory-clause"),
@@ -43,6 +45,18 @@ VARIANTS = {
     "d3": ("-DNMP_WAVES_PER_EU_F64=3",),
     "mlicm": ("-mllvm", "-disable-machine-licm=false"),
     "w4_mlicm": ("-DNMP_WAVES_PER_EU=4", "-mllvm", "-disable-machine-licm=false"),
+    "split_speed": ("-mllvm", "-split-spill-mode=speed"),
+    "split_size": ("-mllvm", "-split-spill-mode=size"),
+    "rptrack": ("-mllvm", "-amdgpu-use-amdgpu-trackers"),
+    "dce_ra": ("-mllvm", "-amdgpu-dce-in-ra"),
+    "nounclust": ("-mllvm", "-amdgpu-disable-unclustered-high-rp-reschedule"),
+    "relaxocc": ("-mllvm", "-amdgpu-schedule-relaxed-occupancy"),
+    "outline_w3": ("-DNMP_MATH_OUTLINE", "-DNMP_WAVES_PER_EU=3"),
+    "lds_work": ("-DNMP_LDS_WORK",),
+    "lds_state": ("-DNMP_LDS_STATE",),
+    # timing probes only (NOT bit-exact): upper bounds of what faster division
+    # / sqrt sequences could save
+    "nocrdiv": ("-fno-hip-fp32-correctly-rounded-divide-sqrt",),
 }
 if __name__ == "__main__":
     names = sys.argv[1:] or list(VARIANTS)
