@@ -316,10 +316,9 @@ int nmp_sflx_column(nmp_engine* eng, nmp_sflx_args* col);
  * always use ocml double.  Default can also be set with NMP_MATH=fast. */
 int nmp_set_math(nmp_engine* eng, int mode);
 
-/* Columns stepped per 64-lane wave: 8..64 (multiple of 8), or 0 (default) to
- * choose per launch: a column set too small to fill every wave slot of the
- * chip is spread over more, partly filled waves (the step is latency-bound,
- * so a SIMD gains from interleaving more waves even at fewer lanes each).
+/* Columns stepped per 64-lane wave: 8..64 (multiple of 8); 0 = 64 (default).
+ * Fewer columns per wave spread a small column set over more, partly filled
+ * waves; measured slower on config #2, kept as a tuning knob.
  * Results do not depend on it. */
 int nmp_set_cols_per_wave(nmp_engine* eng, int cpw);
 

@@ -48,20 +48,11 @@ int ensure_device(int dev) {
   return NMP_OK;
 }
 
-// Columns per wave.  A launch whose columns give fewer waves than the chip
-// holds at the kernel's occupancy (4 waves/SIMD fp32, 2 fp64) leaves the
-// latency-bound step with nothing to overlap: one wave per SIMD at 65,536
-// columns (config #2).  Spreading the columns over more, partly filled waves
-// lets the SIMD interleave them; the kernel is latency- not issue-bound, so
-// the idle lanes cost little.  Rule: the smallest multiple of 8 (>= 8) that
-// still fills every wave slot, capped at 64.
-int cols_per_wave(const nmp_engine* e, int64_t ncol) {
-  if (e->cpw) return e->cpw;
-  const int64_t slots = (int64_t)e->simds * (e->precision == 4 ? 4 : 2);
-  int64_t c = (ncol + slots - 1) / slots;
-  c = (c + 7) / 8 * 8;
-  return (int)(c < 8 ? 8 : c > 64 ? 64 : c);
-}
+// Columns per wave: 64 unless set.  Fewer columns per wave (more, partly
+// filled waves for a small column set) was measured slower on config #2
+// (65,536 fp64 columns: 0.158 ms per step at 64, 0.209 at 32, 0.361 at 16,
+// DESIGN.md "Small column sets"): the step is not purely latency-bound there.
+int cols_per_wave(const nmp_engine* e, int64_t /*ncol*/) { return e->cpw ? e->cpw : 64; }
 
 template <class T>
 void fill_args(nmp::KArgs<T>& a, const nmp_engine* e, int64_t ncol, int64_t ld,

@@ -83,7 +83,7 @@ class Engine:
         self.set_math(math)
 
     def set_cols_per_wave(self, cpw: int):
-        """nmp_set_cols_per_wave: 8..64 columns per wave, 0 = automatic."""
+        """nmp_set_cols_per_wave: 8..64 columns per wave, 0 = 64 (default)."""
         _lib.check(self._lib.nmp_set_cols_per_wave(self._h, int(cpw)), "nmp_set_cols_per_wave")
 
     def set_math(self, mode: int):

@@ -417,16 +417,16 @@ def test_cols_per_wave_bit_identical(engines, cpw):
     assert ok.all(), (~ok).sum()
 
 
-def test_small_column_set_auto_cols_per_wave(engines):
-    """The automatic choice for a small set (65,536 fp64 columns: 32 per wave)
-    gives the same bits as full waves."""
+def test_small_column_set_cols_per_wave_fp64(engines):
+    """A small fp64 set (65,536 columns) at 32 columns per wave gives the same
+    bits as full waves."""
     from noahmp_amd.engine import ColumnState, Engine
     from noahmp_amd.params import Params
     n = 65536
     cols = cases.make_columns(n, "mixed", Params.builtin().as_dict(), seed=9, julian=120.0)
     f = torch.as_tensor(cases.forcing_step(cols, 120.0, 366, 0, seed=9), device=DEV).double()
     out = []
-    for cpw in (0, 64):
+    for cpw in (32, 64):
         eng = Engine(Params.builtin(), L.CASE_NML_OPTIONS, device=0, precision=8)
         eng.set_cols_per_wave(cpw)
         cs = ColumnState.from_host(cols, DEV, torch.float64)

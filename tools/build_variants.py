@@ -30,6 +30,7 @@ VARIANTS = {
     "w4_b64": ("-DNMP_WAVES_PER_EU=4", "-DNMP_BLOCK=64"),
     "w5": ("-DNMP_WAVES_PER_EU=5",),
     "d1": ("-DNMP_WAVES_PER_EU_F64=1",),
+    "w2_d1": ("-DNMP_WAVES_PER_EU=2", "-DNMP_WAVES_PER_EU_F64=1"),
     "en_w4": ("-DNMP_TRUNC_ENERGY",),
     "en_w5": ("-DNMP_TRUNC_ENERGY", "-DNMP_WAVES_PER_EU=5"),
     "en_w3": ("-DNMP_TRUNC_ENERGY", "-DNMP_WAVES_PER_EU=3"),
