@@ -54,6 +54,14 @@ int ensure_device(int dev) {
 // DESIGN.md "Small column sets"): the step is not purely latency-bound there.
 int cols_per_wave(const nmp_engine* e, int64_t /*ncol*/) { return e->cpw ? e->cpw : 64; }
 
+// Small launches take the half-occupancy kernel (sflx_kernel.hip SMALL): a
+// launch whose waves fit in the slots that kernel leaves (one fp64 / two fp32
+// waves per SIMD) gains nothing from the higher occupancy and pays its spills.
+bool small_launch(const nmp_engine* e, int64_t ncol) {
+  const int64_t waves = (ncol + cols_per_wave(e, ncol) - 1) / cols_per_wave(e, ncol);
+  return waves <= (int64_t)e->simds * (e->precision == 4 ? 2 : 1);
+}
+
 template <class T>
 void fill_args(nmp::KArgs<T>& a, const nmp_engine* e, int64_t ncol, int64_t ld,
                const float zsoil[4], float dt, float julian, int32_t yearlen, void* state,
@@ -94,13 +102,14 @@ int launch(const nmp_engine* e, int64_t ncol, int64_t ld, const float zsoil[4], 
     nmp::KArgs<float> a;
     fill_args(a, e, ncol, ld, zsoil, dt, julian, yearlen, state, isnow, sf, si, fc, diag,
               diag_level, status, order, cost);
-    err = (e->math == 0) ? nmp::launch_sflx<float, true>(e->dparams, a, stream)
-                         : nmp::launch_sflx<float, false>(e->dparams, a, stream);
+    const bool small = small_launch(e, ncol);
+    err = (e->math == 0) ? nmp::launch_sflx<float, true>(e->dparams, a, stream, small)
+                         : nmp::launch_sflx<float, false>(e->dparams, a, stream, small);
   } else {
     nmp::KArgs<double> a;
     fill_args(a, e, ncol, ld, zsoil, dt, julian, yearlen, state, isnow, sf, si, fc, diag,
               diag_level, status, order, cost);
-    err = nmp::launch_sflx<double, false>(e->dparams, a, stream);
+    err = nmp::launch_sflx<double, false>(e->dparams, a, stream, small_launch(e, ncol));
   }
   return err == hipSuccess ? NMP_OK : NMP_E_DEVICE;
 }

@@ -47,7 +47,8 @@ struct KArgs {
 };
 
 template <class T, bool R>
-hipError_t launch_sflx(const DevParams* dparams, const KArgs<T>& a, hipStream_t stream);
+hipError_t launch_sflx(const DevParams* dparams, const KArgs<T>& a, hipStream_t stream,
+                       bool small);
 
 // csrc/rebin.hip: per-tile counting sort of the columns by cost key
 hipError_t launch_rebin(const uint8_t* cost, int32_t* order, int64_t ncol, int tile,

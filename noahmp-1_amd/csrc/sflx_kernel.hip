@@ -2744,21 +2744,30 @@ DEV void sflx_column(const DevParams& P, const KArgs<T>& A, Col<T>& c, const Sin
 }
 
 // ---------------------------------------------------------------------------
-template <class T, bool R>
 // Occupancy target: 4 waves/SIMD for fp32 (128 VGPRs), 2 for fp64 (256).  With
 // the launch tails overlapped by two stream ranges (engine.StreamShards) 4 waves
 // measured 1,175 Mcs/s against 1,131 at 3 (168 VGPRs, fewer spills), 921 at 2
 // and 930 at 5 (tools/sweep.sh; DESIGN.md "Occupancy").  fp64 on config #5
 // (global grid, carbon on): 645 Mcs/s at 2 waves, 534 at 3, 453 at 1 (no
 // spills, 378 VGPRs) (tools/configs.sh).
+// SMALL: the same kernel at half that occupancy (2 fp32 / 1 fp64, fewer or no
+// spills) for launches whose columns cannot fill more wave slots anyway:
+// config #2's 65,536 columns are one wave per SIMD (DESIGN.md "Small column
+// sets": fp64 0.158 -> 0.150 ms per step, fp32 0.130 -> 0.113).
 #ifndef NMP_WAVES_PER_EU
 #define NMP_WAVES_PER_EU 4
 #endif
 #ifndef NMP_WAVES_PER_EU_F64
 #define NMP_WAVES_PER_EU_F64 2
 #endif
+template <class T>
+constexpr int waves_per_eu(bool small) {
+  return sizeof(T) == 4 ? (small ? NMP_WAVES_PER_EU / 2 : NMP_WAVES_PER_EU)
+                        : (small ? (NMP_WAVES_PER_EU_F64 + 1) / 2 : NMP_WAVES_PER_EU_F64);
+}
+template <class T, bool R, bool SMALL>
 __global__ __launch_bounds__(NMP_BLOCK)
-__attribute__((amdgpu_waves_per_eu(sizeof(T) == 4 ? NMP_WAVES_PER_EU : NMP_WAVES_PER_EU_F64)))
+__attribute__((amdgpu_waves_per_eu(waves_per_eu<T>(SMALL))))
 void sflx_step_kernel(const DevParams* __restrict__ gparams,
                                                           KArgs<T> a) {
   __shared__ __attribute__((aligned(16))) DevParams sp;
@@ -2837,13 +2846,19 @@ void sflx_step_kernel(const DevParams* __restrict__ gparams,
 
 // launch wrapper (one instantiation per precision / math policy)
 template <class T, bool R>
-hipError_t launch_sflx(const DevParams* dparams, const KArgs<T>& a, hipStream_t stream) {
+hipError_t launch_sflx(const DevParams* dparams, const KArgs<T>& a, hipStream_t stream,
+                       bool small) {
   const int64_t cols_per_block = (int64_t)(NMP_BLOCK / 64) * a.cpw;
   const int64_t grid = (a.ncol + cols_per_block - 1) / cols_per_block;
   const int block = NMP_BLOCK;
   if (grid == 0) return hipSuccess;
-  hipLaunchKernelGGL((sflx_step_kernel<T, R>), dim3((unsigned)grid), dim3(block), 0, stream,
-                     dparams, a);
+  // the fast-math fp32 path has no small instantiation (code size)
+  if (small && (sizeof(T) == 8 || R))
+    hipLaunchKernelGGL((sflx_step_kernel<T, R, (sizeof(T) == 8 || R)>), dim3((unsigned)grid),
+                       dim3(block), 0, stream, dparams, a);
+  else
+    hipLaunchKernelGGL((sflx_step_kernel<T, R, false>), dim3((unsigned)grid), dim3(block), 0,
+                       stream, dparams, a);
   return hipGetLastError();
 }
 
@@ -2859,8 +2874,11 @@ extern "C" int nmp_debug_phase_cycles(unsigned long long* out16, int reset) {
   return 0;
 }
 #endif
-template hipError_t launch_sflx<float, true>(const DevParams*, const KArgs<float>&, hipStream_t);
-template hipError_t launch_sflx<float, false>(const DevParams*, const KArgs<float>&, hipStream_t);
-template hipError_t launch_sflx<double, false>(const DevParams*, const KArgs<double>&, hipStream_t);
+template hipError_t launch_sflx<float, true>(const DevParams*, const KArgs<float>&, hipStream_t,
+                                             bool);
+template hipError_t launch_sflx<float, false>(const DevParams*, const KArgs<float>&, hipStream_t,
+                                              bool);
+template hipError_t launch_sflx<double, false>(const DevParams*, const KArgs<double>&, hipStream_t,
+                                               bool);
 
 }  // namespace nmp
