@@ -89,6 +89,11 @@ def parse():
                          "the rank that writes LDASOUT (what the offline driver does); 'all' "
                          "all-gathers to every rank")
     ap.add_argument("--period", type=int, default=48, help="resident forcing slices (cycled)")
+    ap.add_argument("--forcing", default="resident", choices=("resident", "device"),
+                    help="resident: --period host-generated forcing slices held in HBM and "
+                         "cycled; device: every step's forcing generated on the device "
+                         "(nmp_forcing_synth, counter-based hash) on each range's stream just "
+                         "before its launch -- the long-run path (config #5, SURVEY 8d)")
     ap.add_argument("--streams", type=int, default=2,
                     help="column ranges stepped on their own HIP streams (overlaps launch tails)")
     ap.add_argument("--order", default="as-generated", choices=("as-generated", "lon", "lon-type"),
@@ -158,10 +163,16 @@ def main():
     build_hash = _nlib.load().nmp_build_hash().decode()  # lib.load refuses a stale library
     cs = ColumnState.from_host(cols, dev, dtype)
     n = cs.ncol
-    F = torch.empty((a.period, L.NFORCING, n), dtype=dtype, device=dev)
-    for s in range(a.period):
-        F[s].copy_(torch.from_numpy(cases.forcing_step(
-            cols, julian0 + s * a.dt / 86400.0, yearlen, s, seed=seed)))
+    if a.forcing == "resident":
+        F = torch.empty((a.period, L.NFORCING, n), dtype=dtype, device=dev)
+        for s in range(a.period):
+            F[s].copy_(torch.from_numpy(cases.forcing_step(
+                cols, julian0 + s * a.dt / 86400.0, yearlen, s, seed=seed)))
+    else:
+        # two forcing buffers: step k writes buffer k % 2 on each range's stream
+        # right before that range's launch (stream order makes reuse safe)
+        F = torch.empty((2, L.NFORCING, n), dtype=dtype, device=dev)
+        clim = torch.as_tensor(cases.climate(cols), device=dev).to(dtype).contiguous()
     gather_dst = 0 if a.gather == "root" else None
     ranges = StreamShards(eng, cs, a.streams, rebin_tile=a.rebin_tile, rebin_every=a.rebin_every)
     comm = torch.cuda.Stream(dev) if use_dist else None
@@ -184,8 +195,15 @@ def main():
         """Bench step k: every column range on its own stream (StreamShards), plus the
         async diagnostics gather on output steps (shard.OutputSchedule)."""
         d = sched.diag_for(k)
-        ranges.step(F[k % a.period], cases.CASE_NML_ZSOIL, a.dt, julian0 + k * a.dt / 86400.0,
-                    yearlen, d, L.DIAG_OUT_LEVEL if d is not None else L.DIAG_NONE, events=ev)
+        jul = julian0 + k * a.dt / 86400.0
+        if a.forcing == "resident":
+            f, pre = F[k % a.period], None
+        else:
+            f = F[k % 2]
+            pre = lambda st, rng: eng.forcing_synth(  # noqa: E731
+                clim, jul, yearlen, seed, k, f, first_col=rank * n, stream=st, cols=rng)
+        ranges.step(f, cases.CASE_NML_ZSOIL, a.dt, jul, yearlen, d,
+                    L.DIAG_OUT_LEVEL if d is not None else L.DIAG_NONE, events=ev, pre=pre)
         sched.finish(k, producers=ranges.streams)
         return d is not None
 
@@ -258,7 +276,7 @@ def main():
             "config": {"workload": workload_name(a, n), "kind": a.kind, "opt_veg": a.opt_veg,
                        "ncol_per_gpu": n,
                        "ncol_total": world * n, "dt_s": a.dt, "out_every": a.out_every,
-                       "math": a.math, "column_order": a.order,
+                       "math": a.math, "column_order": a.order, "forcing": a.forcing,
                        "streams": len(ranges.ranges), "cols_per_wave": a.cpw or "auto",
                        "rebin": {"tile": a.rebin_tile, "every": a.rebin_every}
                        if a.rebin_tile else None,

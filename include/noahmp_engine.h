@@ -134,6 +134,13 @@ enum { NMP_I_VEGTYP = 0, NMP_I_SOILTYP, NMP_I_SLOPETYP, NMP_I_SOILCOLOR, NMP_I_I
 enum { NMP_A_SFCTMP = 0, NMP_A_SFCPRS, NMP_A_PSFC, NMP_A_UU, NMP_A_VV, NMP_A_Q2, NMP_A_SOLDN,
        NMP_A_LWDN, NMP_A_PRCP, NMP_A_COSZ, NMP_A_CO2AIR, NMP_A_O2AIR, NMP_NFORCING };
 
+/* Per-column climate record of the synthetic forcing generator
+ * (nmp_forcing_synth): latitude / longitude (radians), mean air temperature
+ * (K), diurnal amplitude (K), relative humidity (0-1), surface pressure (Pa),
+ * mean wind u / v (m/s), precipitation probability per step. */
+enum { NMP_CLIM_LAT = 0, NMP_CLIM_LON, NMP_CLIM_T0, NMP_CLIM_AMP, NMP_CLIM_RH, NMP_CLIM_PRES,
+       NMP_CLIM_WIND_U, NMP_CLIM_WIND_V, NMP_CLIM_WET, NMP_NCLIM };
+
 /* Full diagnostics = the 58 intent(out) args of noahmp_sflx in dummy order (:82-91). */
 enum {
   NMP_D_FSA = 0, NMP_D_FSR, NMP_D_FIRA, NMP_D_FSH, NMP_D_SSOIL, NMP_D_FCEV,
@@ -268,6 +275,18 @@ int nmp_rebin(nmp_engine* eng, int64_t ncol, const uint8_t* cost, int32_t* order
  * (elements, real type; forcing_period 0 = nsteps distinct slices), julian
  * advancing by dt/86400 per step (julian0 + (float)s*dt/86400.0f); bitwise the
  * same as nsteps nmp_step calls.  diag (if non-NULL) receives the last step only. */
+/* Synthetic forcing for one step, generated on the device (no reference
+ * counterpart: the reference reads LDASIN files, run/case.nml:6-7, and ships
+ * none).  Writes the 12 NMP_A_* fields of ncol columns
+ * (SoA, leading dimension ld, engine precision) from their NMP_CLIM_* climate
+ * records: a diurnal temperature cycle at local solar time, solar geometry,
+ * cloud, humidity, wind and precipitation, with every random draw a
+ * counter-based hash of (seed, step, first_col + column, draw).  Stateless:
+ * any step of any column can be generated on its own, on any rank. */
+int nmp_forcing_synth(nmp_engine* eng, int64_t ncol, int64_t ld, const void* climate,
+                      double julian, int32_t yearlen, uint64_t seed, int64_t step,
+                      int64_t first_col, void* forcing, void* stream);
+
 int nmp_run(nmp_engine* eng, int64_t ncol, int64_t ld, const float zsoil[4], float dt,
             float julian0, int32_t yearlen, int32_t nsteps, void* state, int32_t* isnow,
             const void* static_f, const int32_t* static_i, const void* forcing,

@@ -363,3 +363,20 @@ def forcing_random(cols: ColumnSet, seed: int = 0) -> np.ndarray:
     f[F("CO2AIR")] = 395.0e-6 * cols.pres
     f[F("O2AIR")] = 0.209 * cols.pres
     return f.astype(np.float32)
+
+
+def climate(cols: ColumnSet, dtype=np.float64) -> np.ndarray:
+    """(NCLIM, n) climate records for the device forcing generator
+    (nmp_forcing_synth, layout.CLIMATE): the per-column parameters that
+    forcing_step draws its diurnal cycle from."""
+    c = np.empty((L.NCLIM, cols.n), np.float64)
+    c[L.CLIMATE.index("LAT")] = cols.static_f[L.STATIC_F.index("LAT")]
+    c[L.CLIMATE.index("LON")] = cols.lon
+    c[L.CLIMATE.index("T0")] = cols.t0
+    c[L.CLIMATE.index("AMP")] = cols.amp
+    c[L.CLIMATE.index("RH")] = cols.rh
+    c[L.CLIMATE.index("PRES")] = cols.pres
+    c[L.CLIMATE.index("WIND_U")] = cols.wind[0]
+    c[L.CLIMATE.index("WIND_V")] = cols.wind[1]
+    c[L.CLIMATE.index("WET")] = cols.wet
+    return c.astype(dtype)

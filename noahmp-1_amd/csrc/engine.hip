@@ -252,6 +252,20 @@ int nmp_rebin(nmp_engine* eng, int64_t ncol, const uint8_t* cost, int32_t* order
              : NMP_E_DEVICE;
 }
 
+int nmp_forcing_synth(nmp_engine* eng, int64_t ncol, int64_t ld, const void* climate,
+                      double julian, int32_t yearlen, uint64_t seed, int64_t step,
+                      int64_t first_col, void* forcing, void* stream) {
+  if (!eng || ncol < 0 || ld < ncol || yearlen <= 0 || step < 0 || first_col < 0) return NMP_E_ARG;
+  if (ncol == 0) return NMP_OK;
+  if (!climate || !forcing) return NMP_E_ARG;
+  if (ensure_device(eng->device) != NMP_OK) return NMP_E_DEVICE;
+  return nmp::launch_forcing_synth(eng->precision, ncol, ld, climate, julian, yearlen, seed, step,
+                                   first_col, forcing, static_cast<hipStream_t>(stream)) ==
+                 hipSuccess
+             ? NMP_OK
+             : NMP_E_DEVICE;
+}
+
 int nmp_run(nmp_engine* eng, int64_t ncol, int64_t ld, const float zsoil[4], float dt,
             float julian0, int32_t yearlen, int32_t nsteps, void* state, int32_t* isnow,
             const void* static_f, const int32_t* static_i, const void* forcing,

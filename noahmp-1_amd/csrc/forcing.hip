@@ -1,0 +1,112 @@
+// Synthetic LDASIN-style forcing generated on the device (SURVEY.md 8d,
+// config #5: "forcing generated on device from a counter-based hash"; a year of
+// hourly forcing for 1 M columns streamed from the host would be 0.4-0.8 TB).
+//
+// The reference reads forcing from LDASIN files (run/case.nml:6-7) and ships
+// none, so the synthetic cases (noahmp-1_amd/cases.py) define their own
+// diurnal climate per column.  This kernel is that generator with its random
+// draws taken from a stateless counter-based hash of (seed, step, column,
+// draw): any step of any column can be produced independently, on any rank,
+// in any order, with no generator state to carry or shard.  Every value is
+// computed in double and rounded once to the engine precision; the numpy
+// restatement in tests/test_gpu_forcing.py follows it operation for operation.
+//
+// Per column, field-major (ld apart): the climate record NMP_CLIM_* (lat and
+// lon in radians, mean temperature, diurnal amplitude, relative humidity,
+// pressure, mean wind u/v, precipitation probability); out: the 12 NMP_A_*
+// forcing fields of one step.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "noahmp_engine.h"
+
+namespace nmp {
+
+__device__ __forceinline__ uint64_t mix64(uint64_t h) {
+  h ^= h >> 30;
+  h *= 0xBF58476D1CE4E5B9ull;
+  h ^= h >> 27;
+  h *= 0x94D049BB133111EBull;
+  h ^= h >> 31;
+  return h;
+}
+
+// uniform in [0, 1): 53 hash bits
+__device__ __forceinline__ double uhash(uint64_t key, uint64_t draw) {
+  return (double)(mix64(key + draw * 0xF1357AEA2E62A9C5ull) >> 11) * 0x1.0p-53;
+}
+
+// standard normal (Box-Muller on draws d, d+1; 1 - u keeps the log finite)
+__device__ __forceinline__ double nhash(uint64_t key, uint64_t d) {
+  const double u1 = 1.0 - uhash(key, d), u2 = uhash(key, d + 1);
+  return sqrt(-2.0 * log(u1)) * cos(6.283185307179586 * u2);
+}
+
+template <class T>
+__global__ __launch_bounds__(256) void forcing_synth_kernel(int64_t ncol, int64_t ld,
+                                                            const T* __restrict__ clim,
+                                                            double julian, int32_t yearlen,
+                                                            uint64_t seed, int64_t step,
+                                                            int64_t first_col,
+                                                            T* __restrict__ out) {
+  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= ncol) return;
+  const double lat = (double)clim[NMP_CLIM_LAT * ld + c];
+  const double lon = (double)clim[NMP_CLIM_LON * ld + c];
+  const double t0 = (double)clim[NMP_CLIM_T0 * ld + c];
+  const double amp = (double)clim[NMP_CLIM_AMP * ld + c];
+  const double rh = (double)clim[NMP_CLIM_RH * ld + c];
+  const double pres = (double)clim[NMP_CLIM_PRES * ld + c];
+  const double wu = (double)clim[NMP_CLIM_WIND_U * ld + c];
+  const double wv = (double)clim[NMP_CLIM_WIND_V * ld + c];
+  const double wet = (double)clim[NMP_CLIM_WET * ld + c];
+  const uint64_t key = seed * 0x9E3779B97F4A7C15ull + (uint64_t)step * 0xD1B54A32D192ED03ull +
+                       (uint64_t)(first_col + c) * 0xAEF17502108EF2D9ull;
+  const double pi = 3.141592653589793;
+  // diurnal temperature at local solar time (cases.forcing_step)
+  const double frac = julian - floor(julian);
+  const double hour = fmod(frac * 24.0 + lon * (180.0 / pi) / 15.0 + 48.0, 24.0);
+  const double t = t0 + amp * cos(2.0 * pi * (hour - 14.0) / 24.0) + 0.3 * nhash(key, 0);
+  // solar geometry (timeman.cosz)
+  const double decl = 0.409 * sin(2.0 * pi * (julian - 80.0) / (double)yearlen);
+  const double ha = 2.0 * pi * frac + lon - pi;
+  const double cz = sin(lat) * sin(decl) + cos(lat) * cos(decl) * cos(ha);
+  const double cloud = 0.6 * uhash(key, 2);
+  const double soldn = (cz > 0.0 ? cz : 0.0) * 1000.0 * (1.0 - 0.6 * cloud);
+  const double lwdn = (0.72 + 0.2 * cloud) * 5.67e-8 * (t * t) * (t * t);
+  const double e = rh * 611.2 * exp(17.67 * (t - 273.15) / (t - 29.65));
+  const double q2 = 0.622 * e / (pres - 0.378 * e);
+  const double prcp = uhash(key, 3) < wet ? -1.0e-3 * log(1.0 - uhash(key, 4)) : 0.0;
+  T* o = out + c;
+  o[NMP_A_SFCTMP * ld] = (T)t;
+  o[NMP_A_SFCPRS * ld] = (T)pres;
+  o[NMP_A_PSFC * ld] = (T)pres;
+  o[NMP_A_UU * ld] = (T)(wu + 0.7 * nhash(key, 5));
+  o[NMP_A_VV * ld] = (T)(wv + 0.7 * nhash(key, 7));
+  o[NMP_A_Q2 * ld] = (T)q2;
+  o[NMP_A_SOLDN * ld] = (T)soldn;
+  o[NMP_A_LWDN * ld] = (T)lwdn;
+  o[NMP_A_PRCP * ld] = (T)prcp;
+  o[NMP_A_COSZ * ld] = (T)cz;
+  o[NMP_A_CO2AIR * ld] = (T)(395.0e-6 * pres);
+  o[NMP_A_O2AIR * ld] = (T)(0.209 * pres);
+}
+
+hipError_t launch_forcing_synth(int precision, int64_t ncol, int64_t ld, const void* clim,
+                                double julian, int32_t yearlen, uint64_t seed, int64_t step,
+                                int64_t first_col, void* out, hipStream_t stream) {
+  const int64_t grid = (ncol + 255) / 256;
+  if (grid == 0) return hipSuccess;
+  if (precision == 4)
+    hipLaunchKernelGGL(forcing_synth_kernel<float>, dim3((unsigned)grid), dim3(256), 0, stream,
+                       ncol, ld, static_cast<const float*>(clim), julian, yearlen, seed, step,
+                       first_col, static_cast<float*>(out));
+  else
+    hipLaunchKernelGGL(forcing_synth_kernel<double>, dim3((unsigned)grid), dim3(256), 0, stream,
+                       ncol, ld, static_cast<const double*>(clim), julian, yearlen, seed, step,
+                       first_col, static_cast<double*>(out));
+  return hipGetLastError();
+}
+
+}  // namespace nmp

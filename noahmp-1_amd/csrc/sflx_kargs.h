@@ -50,6 +50,11 @@ template <class T, bool R>
 hipError_t launch_sflx(const DevParams* dparams, const KArgs<T>& a, hipStream_t stream,
                        bool small);
 
+// csrc/forcing.hip: synthetic forcing of one step from the climate records
+hipError_t launch_forcing_synth(int precision, int64_t ncol, int64_t ld, const void* clim,
+                                double julian, int32_t yearlen, uint64_t seed, int64_t step,
+                                int64_t first_col, void* out, hipStream_t stream);
+
 // csrc/rebin.hip: per-tile counting sort of the columns by cost key
 hipError_t launch_rebin(const uint8_t* cost, int32_t* order, int64_t ncol, int tile,
                         hipStream_t stream);

@@ -170,6 +170,26 @@ class Engine:
         _lib.check(self._lib.nmp_rebin(self._h, hi - lo, _ptr(cost, lo), _ptr(order, lo),
                                        int(tile), C.c_void_p(s.cuda_stream)), "nmp_rebin")
 
+    def forcing_synth(self, climate: torch.Tensor, julian: float, yearlen: int, seed: int,
+                      step: int, out: torch.Tensor, first_col: int = 0, stream=None,
+                      cols: tuple[int, int] | None = None):
+        """nmp_forcing_synth: one step of synthetic forcing, generated on the
+        device from the (NCLIM, n) climate records into out (NFORCING, n);
+        cols=(lo, hi) generates only those columns (first_col + lo is their
+        global index, so ranges and ranks draw the same numbers as one launch)."""
+        n = int(climate.shape[1])
+        lo, hi = (0, n) if cols is None else (int(cols[0]), int(cols[1]))
+        assert climate.shape == (L.NCLIM, n) and climate.dtype == self.dtype
+        assert out.shape == (L.NFORCING, n) and out.dtype == self.dtype
+        assert climate.is_contiguous() and out.is_contiguous()
+        for t in (climate, out):
+            assert t.device.type == "cuda" and t.device.index == self.device
+        s = stream if stream is not None else torch.cuda.current_stream(self.device)
+        _lib.check(self._lib.nmp_forcing_synth(self._h, hi - lo, n, _ptr(climate, lo),
+                                               float(julian), int(yearlen), int(seed) & (2**64 - 1),
+                                               int(step), int(first_col) + lo, _ptr(out, lo),
+                                               C.c_void_p(s.cuda_stream)), "nmp_forcing_synth")
+
     def sflx_columns(self, rec: np.ndarray) -> np.ndarray:
         """noahmp_sflx with the reference calling sequence on host records
         (layout.sflx_args_dtype(); nmp_sflx_columns), updated in place and returned.
@@ -249,13 +269,15 @@ class StreamShards:
 
     def step(self, forcing: torch.Tensor, zsoil, dt: float, julian: float, yearlen: int,
              diag: torch.Tensor | None = None, diag_level: int = L.DIAG_NONE, events=None,
-             after: torch.cuda.Stream | None | str = "current"):
+             after: torch.cuda.Stream | None | str = "current", pre=None):
         """One step of every range.  `after`: the stream whose pending work (the
         forcing upload, a previous reader of `diag`) each range waits for first
         -- by default the caller's current stream, where torch enqueues uploads;
         tensors are kept alive until the ranges are done with them.  Pass None
         only when the inputs are known to be complete (e.g. after a synchronize).
-        events: per-range (start, end) pairs."""
+        events: per-range (start, end) pairs.  pre(stream, (lo, hi)): work
+        enqueued on each range's stream before its step (e.g. generating that
+        range's forcing on the device, Engine.forcing_synth)."""
         if after == "current":
             after = torch.cuda.current_stream(self.streams[0].device)
         for i, (st, rng) in enumerate(zip(self.streams, self.ranges)):
@@ -264,6 +286,8 @@ class StreamShards:
                 forcing.record_stream(st)
                 if diag is not None:
                     diag.record_stream(st)
+            if pre is not None:
+                pre(st, rng)
             if events is not None:
                 events[i][0].record(st)
             if self.rebin_tile and self.nstep > 0 and self.nstep % self.rebin_every == 0:

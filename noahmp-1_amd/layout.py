@@ -140,6 +140,9 @@ assert NSTATE == 56
 NSTATIC_F = len(STATIC_F)
 NSTATIC_I = len(STATIC_I)
 NFORCING = len(FORCING)
+# climate record of the device forcing generator (NMP_CLIM_*, nmp_forcing_synth)
+CLIMATE = ["LAT", "LON", "T0", "AMP", "RH", "PRES", "WIND_U", "WIND_V", "WET"]
+NCLIM = len(CLIMATE)
 NDIAG_FULL = len(DIAG_FULL)
 NDIAG_OUT = len(DIAG_OUT)
 assert NDIAG_FULL == 58 and NDIAG_OUT == 16

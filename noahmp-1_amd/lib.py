@@ -96,6 +96,8 @@ def load(build_if_missing: bool = False):
     lib.nmp_step_binned.argtypes = [vp, C.c_int64, C.c_int64, f32p, C.c_float, C.c_float,
                                      C.c_int32, vp, vp, vp, vp, vp, vp, C.c_int, vp, vp, vp, vp]
     lib.nmp_rebin.argtypes = [vp, C.c_int64, vp, vp, C.c_int32, vp]
+    lib.nmp_forcing_synth.argtypes = [vp, C.c_int64, C.c_int64, vp, C.c_double, C.c_int32,
+                                      C.c_uint64, C.c_int64, C.c_int64, vp, vp]
     lib.nmp_run.argtypes = [vp, C.c_int64, C.c_int64, f32p, C.c_float, C.c_float, C.c_int32,
                             C.c_int32, vp, vp, vp, vp, vp, C.c_int64, C.c_int32, vp, C.c_int, vp,
                             vp]
@@ -119,7 +121,7 @@ def load(build_if_missing: bool = False):
     return lib
 
 
-EXPORTED_SYMBOLS = ["nmp_read_tables", "nmp_init", "nmp_step", "nmp_step_binned", "nmp_rebin",
+EXPORTED_SYMBOLS = ["nmp_read_tables", "nmp_init", "nmp_step", "nmp_step_binned", "nmp_rebin", "nmp_forcing_synth",
                     "nmp_run", "nmp_run_out",
                     "nmp_state_from_aos", "nmp_sflx_columns", "nmp_sflx_column",
                     "nmp_engine_info", "nmp_set_math", "nmp_set_cols_per_wave", "nmp_finalize", "nmp_strerror",
