@@ -46,9 +46,10 @@ def test_device_forcing_matches_restatement(engine_lib, precision):
         # the rain decision is an exact comparison of hash bits: identical
         assert np.array_equal(got[F("PRCP")] > 0, want[F("PRCP")] > 0)
         # ocml vs glibc double libm differ by <= 1 ulp of double: after the
-        # rounding to the engine precision a few ulp at most
-        tol = 4e-6 if precision == 4 else 1e-12
-        np.testing.assert_allclose(got, want, rtol=tol, atol=tol * 1e-2)
+        # rounding to fp32 a few ulp at most; in fp64 the ulp survives, and
+        # sums that cancel (COSZ near the terminator) amplify it relatively
+        rtol, atol = (4e-6, 4e-8) if precision == 4 else (1e-10, 1e-12)
+        np.testing.assert_allclose(got, want, rtol=rtol, atol=atol)
     eng.close()
 
 
