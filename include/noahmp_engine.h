@@ -308,7 +308,12 @@ int nmp_run_out(nmp_engine* eng, int64_t ncol, int64_t ld, const float zsoil[4],
 /* Host-side converter: n byte-identical `noahmp_state_t` sequence records
  * (168 B each, core/module_noahmp_type.f90:10-42) -> host SoA float state
  * (ld >= n) + isnow, applying the unit/sign mapping of SURVEY.md 8b.
- * Fields the record lacks are left untouched. */
+ * Fields the record lacks are left untouched.
+ * PARITY-UNPINNED: no reference code reads or writes noahmp_state_t, so the
+ * record's conventions are taken from its field comments alone
+ * (core/module_noahmp_type.f90:18,33,41): snowwat is read as mm (kg m-2)
+ * although the comment says kg m-3, zsnow as layer tops above ground, zwt as
+ * height (+up).  Only the byte layout is tested (tests/test_abi_host.py). */
 int nmp_state_from_aos(const void* records, int64_t n, int64_t ld, float* state, int32_t* isnow,
                        int32_t* static_i);
 
@@ -319,9 +324,9 @@ int nmp_state_from_aos(const void* records, int64_t n, int64_t ld, float* state,
  * columns (the per-column entry SURVEY 8b names nmp_sflx_column).
  *  - nsoil must be 4 and nsnow 3; dt, julian, yearlen and zsoil must be the
  *    same in every record of one call (they are launch-wide), else NMP_E_ARG.
- *  - FICEOLD: the engine derives it from SNICE/SNLIQ at step start, as the
- *    offline and WRF drivers compute it; a record whose FICEOLD of an active
- *    snow layer differs from SNICE/(SNICE+SNLIQ) is rejected (NMP_E_ARG).
+ *  - FICEOLD is taken as the record carries it, like noahmp_sflx's
+ *    intent(in) argument (the SoA nmp_step path derives it from SNICE/SNLIQ
+ *    at step start instead, as the offline and WRF drivers compute it).
  *  - iloc, jloc, dx, dz8w, qc, pblh and iz0tlnd never enter the arithmetic
  *    (SURVEY H9); zlvl is intent(inout) but never modified, as in the reference.
  *  - status receives the column's NMP_ST_* bits (0 = the reference would not

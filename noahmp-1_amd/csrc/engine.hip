@@ -66,7 +66,8 @@ template <class T>
 void fill_args(nmp::KArgs<T>& a, const nmp_engine* e, int64_t ncol, int64_t ld,
                const float zsoil[4], float dt, float julian, int32_t yearlen, void* state,
                int32_t* isnow, const void* sf, const int32_t* si, const void* fc, void* diag,
-               int diag_level, int32_t* status, const int32_t* order, uint8_t* cost) {
+               int diag_level, int32_t* status, const int32_t* order, uint8_t* cost,
+               const void* ficeold) {
   a.ncol = ncol;
   a.ld = ld;
   for (int k = 0; k < 4; ++k) a.zsoil[k] = zsoil[k];
@@ -90,25 +91,27 @@ void fill_args(nmp::KArgs<T>& a, const nmp_engine* e, int64_t ncol, int64_t ld,
   a.status = status;
   a.order = order;
   a.cost = cost;
+  a.ficeold = static_cast<const T*>(ficeold);
   a.cpw = cols_per_wave(e, ncol);
 }
 
 int launch(const nmp_engine* e, int64_t ncol, int64_t ld, const float zsoil[4], float dt,
            float julian, int32_t yearlen, void* state, int32_t* isnow, const void* sf,
            const int32_t* si, const void* fc, void* diag, int diag_level, int32_t* status,
-           hipStream_t stream, const int32_t* order = nullptr, uint8_t* cost = nullptr) {
+           hipStream_t stream, const int32_t* order = nullptr, uint8_t* cost = nullptr,
+           const void* ficeold = nullptr) {
   hipError_t err;
   if (e->precision == 4) {
     nmp::KArgs<float> a;
     fill_args(a, e, ncol, ld, zsoil, dt, julian, yearlen, state, isnow, sf, si, fc, diag,
-              diag_level, status, order, cost);
+              diag_level, status, order, cost, ficeold);
     const bool small = small_launch(e, ncol);
     err = (e->math == 0) ? nmp::launch_sflx<float, true>(e->dparams, a, stream, small)
                          : nmp::launch_sflx<float, false>(e->dparams, a, stream, small);
   } else {
     nmp::KArgs<double> a;
     fill_args(a, e, ncol, ld, zsoil, dt, julian, yearlen, state, isnow, sf, si, fc, diag,
-              diag_level, status, order, cost);
+              diag_level, status, order, cost, ficeold);
     err = nmp::launch_sflx<double, false>(e->dparams, a, stream, small_launch(e, ncol));
   }
   return err == hipSuccess ? NMP_OK : NMP_E_DEVICE;
@@ -384,11 +387,12 @@ namespace {
 template <class T>
 struct SflxPack {
   int64_t n;
-  std::vector<T> st, sf, fc, dg;
+  std::vector<T> st, sf, fc, dg, fo;
   std::vector<int32_t> isn, si, status;
   explicit SflxPack(int64_t n_)
       : n(n_), st(NMP_NSTATE * n_), sf(NMP_NSTATIC_F * n_), fc(NMP_NFORCING * n_),
-        dg(NMP_NDIAG_FULL * n_), isn(n_), si(NMP_NSTATIC_I * n_), status(n_, 0) {}
+        dg(NMP_NDIAG_FULL * n_), fo(NMP_NSNOW * n_), isn(n_), si(NMP_NSTATIC_I * n_),
+        status(n_, 0) {}
   T& S(int f, int64_t c) { return st[f * n + c]; }
 
   void pack(const nmp_sflx_args& r, int64_t c) {
@@ -399,6 +403,7 @@ struct SflxPack {
     for (int j = 0; j < NMP_NSNOW; ++j) {
       S(NMP_S_SNICE + j, c) = r.snice[j];
       S(NMP_S_SNLIQ + j, c) = r.snliq[j];
+      fo[j * n + c] = r.ficeold[j];  // the caller's FICEOLD, as noahmp_sflx takes it
     }
     for (int k = 0; k < NMP_NSOIL; ++k) {
       S(NMP_S_SH2O + k, c) = r.soilwat[k];
@@ -457,17 +462,14 @@ int sflx_columns(nmp_engine* eng, nmp_sflx_args* cols, int64_t n) {
       return NMP_E_ARG;
     for (int k = 0; k < NMP_NSOIL; ++k)
       if (!same_f(r.zsoil[k], r0.zsoil[k])) return NMP_E_ARG;
-    // FICEOLD of the active snow layers must be the step-start ice fraction the
-    // engine derives (func.f90:5655 reads only those before a new layer exists)
-    for (int j = r.isnow + 3; j < NMP_NSNOW; ++j)
-      if (!same_f(r.ficeold[j], r.snice[j] / (r.snice[j] + r.snliq[j]))) return NMP_E_ARG;
   }
   SflxPack<T> h(n);
   for (int64_t c = 0; c < n; ++c) h.pack(cols[c], c);
   const size_t nb_st = h.st.size() * sizeof(T), nb_sf = h.sf.size() * sizeof(T),
                nb_fc = h.fc.size() * sizeof(T), nb_dg = h.dg.size() * sizeof(T),
                nb_i = (size_t)n * sizeof(int32_t);
-  const size_t total = nb_st + nb_sf + nb_fc + nb_dg + nb_i * (2 + NMP_NSTATIC_I);
+  const size_t nb_fo = h.fo.size() * sizeof(T);
+  const size_t total = nb_st + nb_sf + nb_fc + nb_dg + nb_fo + nb_i * (2 + NMP_NSTATIC_I);
   char* d = nullptr;
   if (hipMalloc(&d, total) != hipSuccess) return NMP_E_DEVICE;
   char* p = d;
@@ -476,6 +478,7 @@ int sflx_columns(nmp_engine* eng, nmp_sflx_args* cols, int64_t n) {
   T* d_sf = reinterpret_cast<T*>(take(nb_sf));
   T* d_fc = reinterpret_cast<T*>(take(nb_fc));
   T* d_dg = reinterpret_cast<T*>(take(nb_dg));
+  T* d_fo = reinterpret_cast<T*>(take(nb_fo));
   int32_t* d_isn = reinterpret_cast<int32_t*>(take(nb_i));
   int32_t* d_status = reinterpret_cast<int32_t*>(take(nb_i));
   int32_t* d_si = reinterpret_cast<int32_t*>(take(nb_i * NMP_NSTATIC_I));
@@ -483,13 +486,14 @@ int sflx_columns(nmp_engine* eng, nmp_sflx_args* cols, int64_t n) {
   if (hipMemcpy(d_st, h.st.data(), nb_st, hipMemcpyHostToDevice) != hipSuccess ||
       hipMemcpy(d_sf, h.sf.data(), nb_sf, hipMemcpyHostToDevice) != hipSuccess ||
       hipMemcpy(d_fc, h.fc.data(), nb_fc, hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(d_fo, h.fo.data(), nb_fo, hipMemcpyHostToDevice) != hipSuccess ||
       hipMemcpy(d_isn, h.isn.data(), nb_i, hipMemcpyHostToDevice) != hipSuccess ||
       hipMemcpy(d_si, h.si.data(), nb_i * NMP_NSTATIC_I, hipMemcpyHostToDevice) != hipSuccess ||
       hipMemset(d_status, 0, nb_i) != hipSuccess || hipMemset(d_dg, 0, nb_dg) != hipSuccess)
     rc = NMP_E_DEVICE;
   if (rc == NMP_OK)
     rc = launch(eng, n, n, r0.zsoil, r0.dt, r0.julian, r0.yearlen, d_st, d_isn, d_sf, d_si, d_fc,
-                d_dg, NMP_DIAG_FULL, d_status, nullptr);
+                d_dg, NMP_DIAG_FULL, d_status, nullptr, nullptr, nullptr, d_fo);
   if (rc == NMP_OK && (hipDeviceSynchronize() != hipSuccess ||
                        hipMemcpy(h.st.data(), d_st, nb_st, hipMemcpyDeviceToHost) != hipSuccess ||
                        hipMemcpy(h.dg.data(), d_dg, nb_dg, hipMemcpyDeviceToHost) != hipSuccess ||

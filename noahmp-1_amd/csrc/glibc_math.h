@@ -13,6 +13,18 @@
 //     e_exp2f.c, e_logf.c, e_powf.c); table-driven, double internal arithmetic.
 //   tanhf/atanf: fdlibm (Sun) float ports (s_tanhf.c + s_expm1f.c, s_atanf.c).
 //
+// Upstream notices (the algorithms and their constants / table values come
+// from these sources; the code here is our own restatement):
+//   ARM optimized-routines expf/exp2f/logf/powf: Copyright (c) 2017-2018, Arm
+//     Limited; MIT License (SPDX-License-Identifier: MIT), as distributed in
+//     glibc 2.35 under the LGPL-2.1-or-later with that notice retained.
+//   fdlibm tanhf/expm1f/atanf/log10f/acosf/tanf float ports: Copyright (C)
+//     1993 by Sun Microsystems, Inc.  "Developed at SunPro, a Sun Microsystems,
+//     Inc. business.  Permission to use, copy, modify, and distribute this
+//     software is freely granted, provided that this notice is preserved."
+//     (float conversions by Ian Lance Taylor, Cygnus Support).
+//   glibc 2.35 (GNU C Library): LGPL-2.1-or-later.
+//
 // Tables are parameters (struct GmTables) so the kernel can stage them in LDS.
 #pragma once
 #include <math.h>

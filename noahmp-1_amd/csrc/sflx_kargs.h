@@ -41,6 +41,9 @@ struct KArgs {
   // order is set; cost (if set) receives each column's loop-cost key
   const int32_t* order;
   uint8_t* cost;
+  // noahmp_sflx's FICEOLD argument (3 x ld), or NULL: derived from
+  // SNICE/SNLIQ at step start (offline-driver convention)
+  const T* ficeold;
   // columns stepped per 64-lane wave (8..64, a multiple of 8): below 64 the
   // launch spreads a small column set over more waves (small-N latency hiding)
   int cpw;

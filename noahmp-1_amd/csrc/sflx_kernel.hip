@@ -898,6 +898,7 @@ struct Sink {
   const T* fc;        // forcing + column
   int32_t* isnow;     // isnow + column
   uint8_t* cost;      // cost key + column (re-binning), or NULL
+  const T* fice;      // caller FICEOLD + column, or NULL
   // late loads: fields first needed deep in the step are read there, not at
   // kernel entry, so they do not hold registers through the energy phase
   DEV T ls(int f) const { return st[f * ld]; }
@@ -1630,10 +1631,17 @@ DEV void sflx_column(const DevParams& P, const KArgs<T>& A, Col<T>& c, const Sin
     }
     layer_dz(c);
   }
-  // FICEOLD from the state at step start (offline-driver convention)
+  // FICEOLD: the caller's (nmp_sflx_columns, noahmp_sflx's intent(in) argument)
+  // or, by default, the state's ice fraction at step start (offline-driver
+  // convention)
+  if (out.fice) {
 #pragma unroll
-  for (int j = 0; j < 3; ++j)
-    c.ficeold[j] = (j >= c.isnow + 3) ? c.snice[j] / (c.snice[j] + c.snliq[j]) : L(0.0);
+    for (int j = 0; j < 3; ++j) c.ficeold[j] = out.fice[j * out.ld];
+  } else {
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+      c.ficeold[j] = (j >= c.isnow + 3) ? c.snice[j] / (c.snice[j] + c.snliq[j]) : L(0.0);
+  }
   NMP_PHASE(1);
   // thermoprop + csnow + tdfcnd: func.f90:1341-1595
 #pragma unroll
@@ -2838,7 +2846,8 @@ void sflx_step_kernel(const DevParams* __restrict__ gparams,
   c.status = 0;
 
   const Sink<T> out{a.diag ? a.diag + c0 : nullptr, a.state + c0, ld, a.diag_level, sf, si, fc,
-                    a.isnow + c0, a.cost ? a.cost + c0 : nullptr};
+                    a.isnow + c0, a.cost ? a.cost + c0 : nullptr,
+                    a.ficeold ? a.ficeold + c0 : nullptr};
   sflx_column<T, R>(sp, a, c, out);
 
   if (c.status != 0) a.status[c0] |= c.status;

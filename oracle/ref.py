@@ -75,6 +75,8 @@ def _load():
         lib.ref_dump_params.argtypes = [f32p, C.c_int32, i32p, C.c_int32]
         lib.ref_sflx_batch.argtypes = [C.c_int32, C.c_float, C.c_int32, C.c_float, f32p,
                                        f32p, i32p, f32p, i32p, f32p, f32p, i32p]
+        if hasattr(lib, "ref_set_ficeold"):
+            lib.ref_set_ficeold.argtypes = [C.c_void_p, C.c_int32]
         if hasattr(lib, "ref_sflx_run"):
             lib.ref_sflx_run.argtypes = [C.c_int32, C.c_int32, C.c_float, C.c_int32, C.c_float,
                                          f32p, f32p, i32p, f32p, i32p, f32p, C.c_int32, f32p, i32p]
@@ -118,10 +120,12 @@ def dump_params() -> dict:
     return out
 
 
-def step(zsoil, dt, yearlen, julian, state, isnow, static_f, static_i, forcing):
+def step(zsoil, dt, yearlen, julian, state, isnow, static_f, static_i, forcing, ficeold=None):
     """One reference noahmp_sflx step for every column.
 
-    SoA inputs (nfield, n) like the engine; returns (state', isnow', diag(58,n), status)."""
+    SoA inputs (nfield, n) like the engine; returns (state', isnow', diag(58,n), status).
+    ficeold (3, n): noahmp_sflx's FICEOLD argument per column (default: the
+    step-start ice fraction of the active snow layers, 0 elsewhere)."""
     lib = _load()
     n = isnow.shape[0]
     st = np.ascontiguousarray(np.asarray(state, np.float32).T)
@@ -131,9 +135,17 @@ def step(zsoil, dt, yearlen, julian, state, isnow, static_f, static_i, forcing):
     fc = np.ascontiguousarray(np.asarray(forcing, np.float32).T)
     dg = np.zeros((n, NDG), np.float32)
     status = np.zeros(n, np.int32)
+    fo = None if ficeold is None else np.ascontiguousarray(np.asarray(ficeold, np.float32).T)
     with _lock:
-        lib.ref_sflx_batch(n, float(dt), int(yearlen), float(julian),
-                           np.ascontiguousarray(zsoil, np.float32), st, isn, sf, si, fc, dg, status)
+        if fo is not None:
+            lib.ref_set_ficeold(fo.ctypes.data, n)
+        try:
+            lib.ref_sflx_batch(n, float(dt), int(yearlen), float(julian),
+                               np.ascontiguousarray(zsoil, np.float32), st, isn, sf, si, fc, dg,
+                               status)
+        finally:
+            if fo is not None:
+                lib.ref_set_ficeold(None, 0)
     return st.T.copy(), isn, dg.T.copy(), status
 
 

@@ -64,6 +64,7 @@ module ref_harness
   use ref_status
   implicit none
   integer, parameter :: NST = 56, NSF = 6, NSI = 6, NFC = 12, NDG = 58
+  real, allocatable :: fice_in(:, :)  ! caller FICEOLD (ref_set_ficeold), else derived
 contains
 
   subroutine ref_set_options(opts) bind(C, name='ref_set_options')
@@ -202,6 +203,21 @@ contains
     end do
   end subroutine ref_sflx_run
 
+  ! Caller-provided FICEOLD (noahmp_sflx's intent(in) argument, func.f90:129):
+  ! ref_set_ficeold(f, n) makes the next batches pass f(:, c) for column c
+  ! instead of the step-start ice fraction; ref_set_ficeold(NULL, 0) resets.
+  subroutine ref_set_ficeold(f, n) bind(C, name='ref_set_ficeold')
+    type(c_ptr), value :: f
+    integer(c_int32_t), value :: n
+    real(c_float), pointer :: fp(:, :)
+    if (allocated(fice_in)) deallocate(fice_in)
+    if (n > 0 .and. c_associated(f)) then
+       call c_f_pointer(f, fp, [3, n])
+       allocate(fice_in(3, n))
+       fice_in = fp
+    end if
+  end subroutine ref_set_ficeold
+
   subroutine one_column(c, dt, yearlen, julian, zsoil_in, s, isn, sf, si, fc, d, stat)
     integer, intent(in) :: c, yearlen
     real, intent(in) :: dt, julian
@@ -240,6 +256,7 @@ contains
     do iz = isn + 1, 0
        ficeold(iz) = snice(iz) / (snice(iz) + snliq(iz))
     end do
+    if (allocated(fice_in)) ficeold = fice_in(:, c)
 
     cur_status = 0
     o = 0.0

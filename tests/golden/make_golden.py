@@ -17,10 +17,13 @@ noahmp_amd.cases.  Each .npz holds inputs AND the reference outputs.
                                 the fixture records its `soil`/`veg` table tags
   traj_combo_a.npz              48 steps (dt=1800 s) of 32 columns under combo_a
                                 (dynamic vegetation + carbon, Chen97 surface layer, ...)
+  ficeold_snow.npz              one call over melting snow columns with a caller FICEOLD
+                                that differs from the step-start ice fraction (compact's
+                                DDZ3, func.f90:5655)
 
 usage (this container only; needs /root/reference):
   make -C oracle ref && python tests/golden/make_golden.py [group ...]
-  groups: params single variants traj combos tables (default: all)
+  groups: params single variants traj combos tables ficeold (default: all)
 """
 from __future__ import annotations
 
@@ -140,7 +143,8 @@ if __name__ == "__main__":
     if len(sys.argv) == 6 and sys.argv[1] == "--table":
         table_child(sys.argv[2], sys.argv[3], sys.argv[4], int(sys.argv[5]))
         sys.exit(0)
-    groups = set(sys.argv[1:]) or {"params", "single", "variants", "traj", "combos", "tables"}
+    groups = set(sys.argv[1:]) or {"params", "single", "variants", "traj", "combos", "tables",
+                                    "ficeold"}
     # the reference keeps tables in process-global module arrays: one process per tag pair
     if "params" in groups:
         for soil, veg in TAGS:
@@ -178,3 +182,27 @@ if __name__ == "__main__":
         for i, (name, soil, veg) in enumerate(TABLE_CASES):
             subprocess.run([sys.executable, __file__, "--table", name, soil, veg, str(400 + i)],
                            check=True)
+    if "ficeold" in groups:
+        # warm steps over snow columns, so layers melt (IMELT = 1) and compaction
+        # reads FICEOLD; the caller's FICEOLD is the step-start fraction scaled
+        # up towards 1 (ice fraction at the previous step, before this melt)
+        ref.configure(BASE)
+        cols = cases.make_columns(2048, "mixed", P, seed=51, julian=100.0)
+        pick = np.nonzero(cols.isnow < 0)[0][:512]
+        cols = cols.take(pick)
+        f = cases.forcing_random(cols, seed=51)
+        f[L.FORCING.index("SFCTMP")] = np.float32(276.0) + np.random.default_rng(52).uniform(
+            0.0, 8.0, cols.n).astype(np.float32)
+        sn_i = cols.state[L.s("SNICE")]
+        sn_l = cols.state[L.s("SNLIQ")]
+        act = np.arange(3)[:, None] >= cols.isnow[None, :] + 3
+        frac = np.where(act, sn_i / np.where(act, sn_i + sn_l, 1.0), 0.0)
+        w = np.random.default_rng(53).uniform(0.0, 1.0, frac.shape)
+        fice = np.where(act, frac + w * (1.0 - frac), 0.0).astype(np.float32)
+        st, isn, dg, status = ref.step(cases.CASE_NML_ZSOIL, 1800.0, 366, 100.3, cols.state,
+                                       cols.isnow, cols.static_f, cols.static_i, f, ficeold=fice)
+        save("ficeold_snow.npz", options=np.array(BASE, np.int32), dt=np.float32(1800.0),
+             julian=np.float32(100.3), yearlen=np.int32(366), zsoil=cases.CASE_NML_ZSOIL,
+             state0=cols.state, isnow0=cols.isnow, static_f=cols.static_f,
+             static_i=cols.static_i, forcing=f, ficeold=fice, state1=st, isnow1=isn, diag=dg,
+             status=status)

@@ -551,8 +551,7 @@ def test_sflx_columns_reference_calling_sequence(engines, name):
 
 
 def test_sflx_columns_rejects_what_the_kernel_cannot_honour(engines):
-    """Launch-wide arguments must agree across records; FICEOLD of an active
-    layer must be the step-start ice fraction (NMP_E_ARG otherwise)."""
+    """Launch-wide arguments must agree across records (NMP_E_ARG otherwise)."""
     from noahmp_amd import lib as _lib
     g = load("single_casenml_mixed.npz")
     eng = engines(g["options"])
@@ -568,11 +567,24 @@ def test_sflx_columns_rejects_what_the_kernel_cannot_honour(engines):
     r["nsoil"][0] = 5
     with pytest.raises(_lib.NmpError):
         eng.sflx_columns(r)
-    r = mk()
-    r["ficeold"][0, 2] = np.float32(0.123)  # layer 0 is active in every snow column
-    with pytest.raises(_lib.NmpError):
-        eng.sflx_columns(r)
     assert eng.sflx_columns(mk()) is not None
+
+
+def test_sflx_columns_caller_ficeold_vs_reference(engines):
+    """nmp_sflx_columns takes FICEOLD as the record carries it (noahmp_sflx's
+    intent(in) argument, func.f90:129): melting snow columns whose caller
+    FICEOLD differs from the step-start ice fraction give the reference's bits
+    (tests/golden/ficeold_snow.npz, made by the reference with that FICEOLD)."""
+    g = load("ficeold_snow.npz")
+    eng = engines(g["options"])
+    r = L.sflx_records(g["state0"], g["isnow0"], g["static_f"], g["static_i"], g["forcing"],
+                       g["zsoil"], g["dt"], g["julian"], g["yearlen"])
+    r["ficeold"][:] = g["ficeold"].T
+    eng.sflx_columns(r)
+    st, isn, dg, status = L.soa_from_records(r)
+    exact = bit_equal(st, g["state1"]).all(0) & bit_equal(dg, g["diag"]).all(0) & \
+        (isn == g["isnow1"]) & (as_ref_status(status) == g["status"])
+    assert exact.all(), f"{(~exact).sum()} of {exact.size} columns differ"
 
 
 @pytest.mark.parametrize("kind,ncol,opt_veg,precision", [
