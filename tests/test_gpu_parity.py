@@ -584,7 +584,10 @@ def test_sflx_columns_caller_ficeold_vs_reference(engines):
     st, isn, dg, status = L.soa_from_records(r)
     exact = bit_equal(st, g["state1"]).all(0) & bit_equal(dg, g["diag"]).all(0) & \
         (isn == g["isnow1"]) & (as_ref_status(status) == g["status"])
-    assert exact.all(), f"{(~exact).sum()} of {exact.size} columns differ"
+    _, rep_s = column_mismatch(st, g["state1"], 0, 0, STATE_NAMES)
+    _, rep_d = column_mismatch(dg, g["diag"], 0, 0, L.DIAG_FULL)
+    assert exact.all(), f"{(~exact).sum()} of {exact.size} columns differ: " + "; ".join(
+        rep_s[:8] + rep_d[:8])
 
 
 @pytest.mark.parametrize("kind,ncol,opt_veg,precision", [
