@@ -73,7 +73,7 @@ def step(P: dict, options, zsoil, dt, yearlen, julian, state, isnow, static_f, s
     correctly rounded libm -- what the engine's default math computes)."""
     lib, rt = _lib(precision)
     n = isnow.shape[0]
-    st = np.ascontiguousarray(np.asarray(state, rt).T)
+    st = np.array(np.asarray(state, rt).T, order="C")  # a copy: written in place
     isn = np.ascontiguousarray(isnow, np.int32).copy()
     sf = np.ascontiguousarray(np.asarray(static_f, rt).T)
     si = np.ascontiguousarray(np.asarray(static_i, np.int32).T)
@@ -110,7 +110,7 @@ def prepare_run(P: dict, options, zsoil, dt, yearlen, julian0, state, isnow, sta
     returns (state', isnow', diag, status) of the last step."""
     lib, rt = _lib(precision)
     n = isnow.shape[0]
-    st = np.ascontiguousarray(np.asarray(state, rt).T)
+    st = np.array(np.asarray(state, rt).T, order="C")  # a copy: written in place
     isn = np.ascontiguousarray(isnow, np.int32).copy()
     sf = np.ascontiguousarray(np.asarray(static_f, rt).T)
     si = np.ascontiguousarray(np.asarray(static_i, np.int32).T)

@@ -128,7 +128,7 @@ def step(zsoil, dt, yearlen, julian, state, isnow, static_f, static_i, forcing, 
     step-start ice fraction of the active snow layers, 0 elsewhere)."""
     lib = _load()
     n = isnow.shape[0]
-    st = np.ascontiguousarray(np.asarray(state, np.float32).T)
+    st = np.array(np.asarray(state, np.float32).T, order="C")  # a copy: written in place
     isn = np.ascontiguousarray(isnow, np.int32).copy()
     sf = np.ascontiguousarray(np.asarray(static_f, np.float32).T)
     si = np.ascontiguousarray(np.asarray(static_i, np.int32).T)
@@ -154,7 +154,7 @@ class Records:
     transposed once, so a timed loop can call `run` without host transposes."""
 
     def __init__(self, state, isnow, static_f, static_i, forcings):
-        self.st = np.ascontiguousarray(np.asarray(state, np.float32).T)
+        self.st = np.array(np.asarray(state, np.float32).T, order="C")  # a copy: written in place
         self.isn = np.ascontiguousarray(isnow, np.int32).copy()
         self.sf = np.ascontiguousarray(np.asarray(static_f, np.float32).T)
         self.si = np.ascontiguousarray(np.asarray(static_i, np.int32).T)

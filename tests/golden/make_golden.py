@@ -190,6 +190,9 @@ if __name__ == "__main__":
         cols = cases.make_columns(2048, "mixed", P, seed=51, julian=100.0)
         pick = np.nonzero(cols.isnow < 0)[0][:512]
         cols = cols.take(pick)
+        cols = cases.ColumnSet(*(np.ascontiguousarray(a) for a in (
+            cols.static_f, cols.static_i, cols.state, cols.isnow, cols.lon, cols.t0, cols.amp,
+            cols.rh, cols.pres, cols.wind, cols.wet)))
         f = cases.forcing_random(cols, seed=51)
         f[L.FORCING.index("SFCTMP")] = np.float32(276.0) + np.random.default_rng(52).uniform(
             0.0, 8.0, cols.n).astype(np.float32)

@@ -167,3 +167,23 @@ def test_reference_run_loop_equals_repeated_steps():
                                        g["static_i"], F[s % 5])
     assert bit_equal(rec.st.T, st).all() and np.array_equal(rec.isn, isn)
     assert bit_equal(rec.dg.T, dg).all()
+
+
+def test_ficeold_fixture_pins_the_caller_argument(oracle_port):
+    """ficeold_snow.npz: the reference run with a caller FICEOLD (harness
+    ref_set_ficeold) differs from the derived-FICEOLD run in the columns whose
+    melting layers compact (func.f90:5655), and the fixture is reproducible."""
+    import ref
+    g = load("ficeold_snow.npz")
+    args = (g["zsoil"], float(g["dt"]), int(g["yearlen"]), float(g["julian"]), g["state0"],
+            g["isnow0"], g["static_f"], g["static_i"], g["forcing"])
+    derived = oracle_port.step(load_params(), tuple(g["options"]), *args)
+    changed = ~bit_equal(derived[0], g["state1"]).all(0)
+    assert 0.05 < changed.mean() < 0.9, changed.mean()  # FICEOLD matters, not everywhere
+    if not ref.available():
+        pytest.skip("reference oracle not built (oracle/_ref)")
+    ref.configure(tuple(g["options"]))
+    st, isn, dg, status = ref.step(*args, ficeold=g["ficeold"])
+    assert bit_equal(st, g["state1"]).all() and bit_equal(dg, g["diag"]).all()
+    st0, *_ = ref.step(*args)
+    assert bit_equal(st0, derived[0]).all()
