@@ -18,7 +18,7 @@ DEFAULT_LIB_PATH = os.path.join(LIB_DIR, "libnoahmp_engine.so")
 # NOAHMP_ENGINE_LIB: a tuning variant (tools/build_variants.py), hash-checked only on request
 LIB_PATH = os.environ.get("NOAHMP_ENGINE_LIB") or DEFAULT_LIB_PATH
 SOURCES = ["engine.hip", "sflx_kernel.hip", "rebin.hip", "forcing.hip", "tables.cpp"]
-HEADERS = ["dev_params.h", "sflx_kargs.h", "sflx_math.h", "glibc_math.h"]
+HEADERS = ["dev_params.h", "sflx_kargs.h", "sflx_math.h", "sflx_routines.h", "glibc_math.h"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")
 FLAGS = ["-O3", f"--offload-arch={ARCH}", "-fPIC", "-shared", "-std=c++17",

@@ -2772,3 +2772,33 @@ int oracle_sflx_run(int32_t n, int32_t nsteps, real dt, int32_t yearlen, real ju
   }
   return 0;
 }
+
+/* ---- single routines, for the per-routine tests (tests/test_gpu_routines.py,
+ * tests/test_oracle_golden.py): the same code sflx_column calls ---- */
+void oracle_esat(int32_t n, const real* t, real* out4) {
+  for (int32_t i = 0; i < n; ++i)
+    esat(t[i], &out4[4 * i], &out4[4 * i + 1], &out4[4 * i + 2], &out4[4 * i + 3]);
+}
+
+void oracle_tdfcnd(const nmp_params* P, int32_t n, const int32_t* sltyp, const real* smc,
+                   const real* sh2o, real* out) {
+  for (int32_t i = 0; i < n; ++i) out[i] = tdfcnd(P, sltyp[i], smc[i], sh2o[i]);
+}
+
+void oracle_frh2o(const nmp_params* P, int32_t n, const int32_t* sltyp, const real* tk,
+                  const real* smc, const real* sh2o, real* out, int32_t* status) {
+  for (int32_t i = 0; i < n; ++i) {
+    ctx_t X = {P, 0, 0};
+    out[i] = frh2o(&X, sltyp[i], tk[i], smc[i], sh2o[i]);
+    status[i] = X.status;
+  }
+}
+
+/* one 7-layer system per column (layers -2..4 as 0..6), solved on layers
+ * kt..6 (NTOP = kt in the 0-based storage); C is updated in place like the
+ * reference's intent(inout) C */
+void oracle_rosr12(int32_t n, const int32_t* kt, const real* a, const real* b, real* c,
+                   const real* d, real* p, real* delta) {
+  for (int32_t i = 0; i < n; ++i)
+    rosr12(p + 7 * i, a + 7 * i, b + 7 * i, c + 7 * i, d + 7 * i, delta + 7 * i, kt[i], 6);
+}

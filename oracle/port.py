@@ -133,3 +133,57 @@ def run(P: dict, options, zsoil, dt, yearlen, julian0, state, isnow, static_f, s
     """nsteps steps over a forcing cycle forcings[(period, 12, n)]."""
     return prepare_run(P, options, zsoil, dt, yearlen, julian0, state, isnow, static_f, static_i,
                        forcings, nsteps, precision)()
+
+
+# ---- single routines (the code sflx_column calls), fp32 bit-exact build ----
+def _rt(name, *argtypes):
+    lib, _ = _lib(4)
+    f = getattr(lib, name)
+    f.argtypes = list(argtypes)
+    f.restype = None
+    return f
+
+
+def esat(t):
+    f32p = np.ctypeslib.ndpointer(np.float32, flags="C_CONTIGUOUS")
+    t = np.ascontiguousarray(t, np.float32)
+    out = np.zeros((t.size, 4), np.float32)
+    _rt("oracle_esat", C.c_int32, f32p, f32p)(t.size, t, out)
+    return out
+
+
+def tdfcnd(P: dict, sltyp, smc, sh2o):
+    f32p = np.ctypeslib.ndpointer(np.float32, flags="C_CONTIGUOUS")
+    i32p = np.ctypeslib.ndpointer(np.int32, flags="C_CONTIGUOUS")
+    n = len(smc)
+    out = np.zeros(n, np.float32)
+    _rt("oracle_tdfcnd", C.c_char_p, C.c_int32, i32p, f32p, f32p, f32p)(
+        pack_params(P), n, np.ascontiguousarray(sltyp, np.int32),
+        np.ascontiguousarray(smc, np.float32), np.ascontiguousarray(sh2o, np.float32), out)
+    return out
+
+
+def frh2o(P: dict, sltyp, tk, smc, sh2o):
+    f32p = np.ctypeslib.ndpointer(np.float32, flags="C_CONTIGUOUS")
+    i32p = np.ctypeslib.ndpointer(np.int32, flags="C_CONTIGUOUS")
+    n = len(tk)
+    out = np.zeros(n, np.float32)
+    st = np.zeros(n, np.int32)
+    _rt("oracle_frh2o", C.c_char_p, C.c_int32, i32p, f32p, f32p, f32p, f32p, i32p)(
+        pack_params(P), n, np.ascontiguousarray(sltyp, np.int32), np.ascontiguousarray(tk, np.float32),
+        np.ascontiguousarray(smc, np.float32), np.ascontiguousarray(sh2o, np.float32), out, st)
+    return out, st
+
+
+def rosr12(kt, a, b, c, d):
+    """(n, 7) systems solved on layers kt..6: returns (p, c', delta)."""
+    f32p = np.ctypeslib.ndpointer(np.float32, flags="C_CONTIGUOUS")
+    i32p = np.ctypeslib.ndpointer(np.int32, flags="C_CONTIGUOUS")
+    n = len(kt)
+    c = np.array(c, np.float32, order="C")
+    p = np.zeros((n, 7), np.float32)
+    dl = np.zeros((n, 7), np.float32)
+    _rt("oracle_rosr12", C.c_int32, i32p, f32p, f32p, f32p, f32p, f32p, f32p)(
+        n, np.ascontiguousarray(kt, np.int32), np.ascontiguousarray(a, np.float32),
+        np.ascontiguousarray(b, np.float32), c, np.ascontiguousarray(d, np.float32), p, dl)
+    return p, c, dl

@@ -75,6 +75,8 @@ def _load():
         lib.ref_dump_params.argtypes = [f32p, C.c_int32, i32p, C.c_int32]
         lib.ref_sflx_batch.argtypes = [C.c_int32, C.c_float, C.c_int32, C.c_float, f32p,
                                        f32p, i32p, f32p, i32p, f32p, f32p, i32p]
+        if hasattr(lib, "ref_frh2o"):
+            lib.ref_frh2o.argtypes = [C.c_int32, i32p, f32p, f32p, f32p, f32p, i32p]
         if hasattr(lib, "ref_set_ficeold"):
             lib.ref_set_ficeold.argtypes = [C.c_void_p, C.c_int32]
         if hasattr(lib, "ref_sflx_run"):
@@ -173,3 +175,17 @@ def run(zsoil, dt, yearlen, julian0, rec: Records, nsteps: int):
                          np.ascontiguousarray(zsoil, np.float32), rec.st, rec.isn, rec.sf, rec.si,
                          rec.fc, rec.fc.shape[0], rec.dg, rec.status)
     return rec
+
+
+def frh2o(sltyp, tk, smc, sh2o):
+    """The reference's public frh2o (func.f90:4494-4598) over arrays (after
+    configure()): (free water, status bits)."""
+    lib = _load()
+    n = len(tk)
+    out = np.zeros(n, np.float32)
+    st = np.zeros(n, np.int32)
+    with _lock:
+        lib.ref_frh2o(n, np.ascontiguousarray(sltyp, np.int32), np.ascontiguousarray(tk, np.float32),
+                      np.ascontiguousarray(smc, np.float32), np.ascontiguousarray(sh2o, np.float32),
+                      out, st)
+    return out, st

@@ -60,7 +60,7 @@ end subroutine wrf_error_fatal
 module ref_harness
   use iso_c_binding
   use noahmp_global
-  use noahmp_func, only: noahmp_sflx
+  use noahmp_func, only: noahmp_sflx, frh2o
   use ref_status
   implicit none
   integer, parameter :: NST = 56, NSF = 6, NSI = 6, NFC = 12, NDG = 58
@@ -217,6 +217,24 @@ contains
        fice_in = fp
     end if
   end subroutine ref_set_ficeold
+
+  ! The reference's one public physics routine besides noahmp_sflx, frh2o
+  ! (func.f90:4494-4598), called directly: per-routine golden values.
+  subroutine ref_frh2o(n, sltyp, tk, smc, sh2o, out, stat) bind(C, name='ref_frh2o')
+    integer(c_int32_t), value :: n
+    integer(c_int32_t), intent(in) :: sltyp(n)
+    real(c_float), intent(in) :: tk(n), smc(n), sh2o(n)
+    real(c_float), intent(out) :: out(n)
+    integer(c_int32_t), intent(out) :: stat(n)
+    integer :: i
+    real :: free
+    do i = 1, n
+       cur_status = 0
+       call frh2o(sltyp(i), free, tk(i), smc(i), sh2o(i))
+       out(i) = free
+       stat(i) = cur_status
+    end do
+  end subroutine ref_frh2o
 
   subroutine one_column(c, dt, yearlen, julian, zsoil_in, s, isn, sf, si, fc, d, stat)
     integer, intent(in) :: c, yearlen

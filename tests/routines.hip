@@ -1,0 +1,164 @@
+// TEST LIBRARY -- per-routine checks of the step kernel's device routines.
+//
+// The step kernel (noahmp-1_amd/csrc/sflx_kernel.hip) is one fused launch, so
+// a bit difference can otherwise only be seen end to end.  This library runs
+// single device routines from csrc/sflx_routines.h -- the SAME code the
+// kernel inlines, in the default fp32 "ref" math -- over arrays of inputs:
+//   esat   func.f90:3692-3736   saturation vapour pressure and derivatives
+//   tdfcnd func.f90:1500-1595   soil thermal conductivity
+//   frh2o  func.f90:4494-4598   supercooled soil water (Newton + Flerchinger)
+//   rosr12 func.f90:4240-4288   tridiagonal (Thomas) solve on layers kt..6
+// tests/test_gpu_routines.py compares them bit for bit with the oracle's C
+// restatement of each routine, and frh2o also with the reference's own
+// (public) frh2o.  Built by __graft_entry__.build() into tests/lib/.
+#include <hip/hip_runtime.h>
+
+#include <vector>
+
+#include "sflx_routines.h"
+
+namespace {
+
+using nmp::DevParams;
+
+__global__ void k_esat(int n, const float* t, float* out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  float esw, esi, desw, desi;
+  nmp::esat<float>(t[i], esw, esi, desw, desi);
+  out[4 * i] = esw;
+  out[4 * i + 1] = esi;
+  out[4 * i + 2] = desw;
+  out[4 * i + 3] = desi;
+}
+
+__global__ void k_tdfcnd(const DevParams* P, int n, const int* sltyp, const float* smc,
+                         const float* sh2o, float* out) {
+  nmp::stage_math_tables();
+  __syncthreads();
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  out[i] = nmp::tdfcnd<float, true>(P->soil[sltyp[i] - 1], smc[i], sh2o[i]);
+}
+
+__global__ void k_frh2o(const DevParams* P, int n, const int* sltyp, const float* tk,
+                        const float* smc, const float* sh2o, float* out, int* status) {
+  nmp::stage_math_tables();
+  __syncthreads();
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const nmp::SoilRec& S = P->soil[sltyp[i] - 1];
+  int st = 0;
+  out[i] = nmp::frh2o<float, true>((float)S.smcmax, (float)S.psisat, (float)S.bexp, tk[i], smc[i],
+                                   sh2o[i], st);
+  status[i] = st;
+}
+
+// one 7-layer system per thread: a, b, c, d in, p (solution) and delta out
+__global__ void k_rosr12(int n, const int* kt, const float* a, const float* b, float* c,
+                         const float* d, float* p, float* delta) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  float pa[7], aa[7], bb[7], cc[7], dd[7], de[7];
+#pragma unroll
+  for (int k = 0; k < 7; ++k) {
+    aa[k] = a[7 * i + k];
+    bb[k] = b[7 * i + k];
+    cc[k] = c[7 * i + k];
+    dd[k] = d[7 * i + k];
+    pa[k] = 0.0f;
+    de[k] = 0.0f;
+  }
+  nmp::rosr12<float, 7>(pa, aa, bb, cc, dd, de, kt[i]);
+#pragma unroll
+  for (int k = 0; k < 7; ++k) {
+    p[7 * i + k] = pa[k];
+    delta[7 * i + k] = de[k];
+    c[7 * i + k] = cc[k];  // intent(inout) in the reference
+  }
+}
+
+// host helpers: device copies in, one launch, results out (synchronous)
+struct Dev {
+  std::vector<void*> ptrs;
+  ~Dev() {
+    for (void* p : ptrs) (void)hipFree(p);
+  }
+  template <class X>
+  X* in(const X* h, size_t n) {
+    void* d = nullptr;
+    if (hipMalloc(&d, n * sizeof(X) + 16) != hipSuccess) return nullptr;
+    ptrs.push_back(d);
+    if (h && hipMemcpy(d, h, n * sizeof(X), hipMemcpyHostToDevice) != hipSuccess) return nullptr;
+    return static_cast<X*>(d);
+  }
+};
+
+int finish(Dev&, float* hout, const float* dout, size_t n) {
+  if (hipDeviceSynchronize() != hipSuccess) return -4;
+  return hipMemcpy(hout, dout, n * sizeof(float), hipMemcpyDeviceToHost) == hipSuccess ? 0 : -4;
+}
+
+const DevParams* dev_params(Dev& D, const nmp_params* p) {
+  DevParams h{};
+  nmp::pack_dev_params(*p, h);
+  return D.in(&h, 1);
+}
+
+}  // namespace
+
+extern "C" {
+
+int rt_esat(int n, const float* t, float* out4) {
+  Dev D;
+  const float* dt = D.in(t, n);
+  float* dout = D.in<float>(nullptr, 4 * (size_t)n);
+  if (!dt || !dout) return -4;
+  hipLaunchKernelGGL(k_esat, dim3((n + 255) / 256), dim3(256), 0, 0, n, dt, dout);
+  return finish(D, out4, dout, 4 * (size_t)n);
+}
+
+int rt_tdfcnd(const nmp_params* p, int n, const int* sltyp, const float* smc, const float* sh2o,
+              float* out) {
+  Dev D;
+  const DevParams* P = dev_params(D, p);
+  const int* ds = D.in(sltyp, n);
+  const float *dm = D.in(smc, n), *dh = D.in(sh2o, n);
+  float* dout = D.in<float>(nullptr, n);
+  if (!P || !ds || !dm || !dh || !dout) return -4;
+  hipLaunchKernelGGL(k_tdfcnd, dim3((n + 255) / 256), dim3(256), 0, 0, P, n, ds, dm, dh, dout);
+  return finish(D, out, dout, n);
+}
+
+int rt_frh2o(const nmp_params* p, int n, const int* sltyp, const float* tk, const float* smc,
+             const float* sh2o, float* out, int* status) {
+  Dev D;
+  const DevParams* P = dev_params(D, p);
+  const int* ds = D.in(sltyp, n);
+  const float *dt = D.in(tk, n), *dm = D.in(smc, n), *dh = D.in(sh2o, n);
+  float* dout = D.in<float>(nullptr, n);
+  int* dst = D.in<int>(nullptr, n);
+  if (!P || !ds || !dt || !dm || !dh || !dout || !dst) return -4;
+  hipLaunchKernelGGL(k_frh2o, dim3((n + 255) / 256), dim3(256), 0, 0, P, n, ds, dt, dm, dh, dout,
+                     dst);
+  if (finish(D, out, dout, n) != 0) return -4;
+  return hipMemcpy(status, dst, n * sizeof(int), hipMemcpyDeviceToHost) == hipSuccess ? 0 : -4;
+}
+
+int rt_rosr12(int n, const int* kt, const float* a, const float* b, float* c, const float* d,
+              float* p, float* delta) {
+  Dev D;
+  const size_t m = 7 * (size_t)n;
+  const int* dk = D.in(kt, n);
+  const float *da = D.in(a, m), *db = D.in(b, m), *dd = D.in(d, m);
+  float* dc = D.in(c, m);
+  float *dp = D.in<float>(nullptr, m), *de = D.in<float>(nullptr, m);
+  if (!dk || !da || !db || !dc || !dd || !dp || !de) return -4;
+  hipLaunchKernelGGL(k_rosr12, dim3((n + 255) / 256), dim3(256), 0, 0, n, dk, da, db, dc, dd, dp,
+                     de);
+  if (finish(D, p, dp, m) != 0) return -4;
+  if (hipMemcpy(c, dc, m * sizeof(float), hipMemcpyDeviceToHost) != hipSuccess) return -4;
+  return hipMemcpy(delta, de, m * sizeof(float), hipMemcpyDeviceToHost) == hipSuccess ? 0 : -4;
+}
+
+}  // extern "C"
