@@ -96,7 +96,8 @@ def parse():
                          "before its launch -- the long-run path (config #5, SURVEY 8d)")
     ap.add_argument("--streams", type=int, default=2,
                     help="column ranges stepped on their own HIP streams (overlaps launch tails)")
-    ap.add_argument("--order", default="as-generated", choices=("as-generated", "lon", "lon-type"),
+    ap.add_argument("--order", default="as-generated",
+                    choices=("as-generated", "lon", "lon-type", "lon-snow-type"),
                     help="column order on the GPU (columns are independent: any permutation "
                          "gives bit-identical per-column results); 'lon' groups columns of "
                          "similar solar time into the same wave, like a real lat-lon grid")
@@ -132,12 +133,8 @@ def main():
     cols = cases.make_columns(a.ncol, a.kind, pdict, seed=seed, julian=julian0,
                               first=rank * a.ncol)
     if a.order != "as-generated":
-        key = np.round(np.degrees(cols.lon) / 2.0)  # 2-degree longitude bands
-        if a.order == "lon-type":
-            perm = np.lexsort((cols.static_i[L.STATIC_I.index("VEGTYP")], key))
-        else:
-            perm = np.argsort(cols.lon, kind="stable")
-        cols = cols.take(perm)
+        from noahmp_amd.order import coherent_order
+        cols = cols.take(coherent_order(cols.lon, cols.static_i, cols.isnow, a.order))
 
     # ---- CPU baseline (rank 0, N=1), BEFORE anything touches the GPU ------
     cpu = None
