@@ -97,10 +97,13 @@ def parse():
     ap.add_argument("--streams", type=int, default=2,
                     help="column ranges stepped on their own HIP streams (overlaps launch tails)")
     ap.add_argument("--order", default="as-generated",
-                    choices=("as-generated", "lon", "lon-type", "lon-snow-type"),
+                    choices=("as-generated", "lon", "lon-type", "lon-snow-type",
+                             "lon-snow-type-soil"),
                     help="column order on the GPU (columns are independent: any permutation "
                          "gives bit-identical per-column results); 'lon' groups columns of "
                          "similar solar time into the same wave, like a real lat-lon grid")
+    ap.add_argument("--order-band", type=float, default=2.0,
+                    help="longitude band (degrees) of the coherent column orders")
     ap.add_argument("--rebin-tile", type=int, default=0,
                     help="column re-binning (nmp_rebin): sort columns by the previous step's "
                          "vege_flux trip count within tiles of this many columns (0 = off)")
@@ -134,7 +137,8 @@ def main():
                               first=rank * a.ncol)
     if a.order != "as-generated":
         from noahmp_amd.order import coherent_order
-        cols = cols.take(coherent_order(cols.lon, cols.static_i, cols.isnow, a.order))
+        cols = cols.take(coherent_order(cols.lon, cols.static_i, cols.isnow, a.order,
+                                        band_deg=a.order_band))
 
     # ---- CPU baseline (rank 0, N=1), BEFORE anything touches the GPU ------
     cpu = None

@@ -13,6 +13,7 @@ Keys, in lexicographic priority (`coherent_order(..., key=...)`):
                    diurnal phase are then shared by a wave)
   "lon-type"       + vegetation type (canopy or not, the canopy's parameters)
   "lon-snow-type"  + snow-covered or not, then vegetation type
+  "lon-snow-type-soil"  + soil type
 A grid already in row-major lat/lon order is mostly coherent; a shuffled
 column set (the bench's config #3) is the worst case.
 """
@@ -22,7 +23,7 @@ import numpy as np
 
 from . import layout as L
 
-KEYS = ("lon", "lon-type", "lon-snow-type")
+KEYS = ("lon", "lon-type", "lon-snow-type", "lon-snow-type-soil")
 
 
 def coherent_order(lon_rad: np.ndarray, static_i: np.ndarray, isnow: np.ndarray,
@@ -36,4 +37,7 @@ def coherent_order(lon_rad: np.ndarray, static_i: np.ndarray, isnow: np.ndarray,
         return np.lexsort((vt, band))
     if key == "lon-snow-type":
         return np.lexsort((vt, np.asarray(isnow) < 0, band))
+    if key == "lon-snow-type-soil":
+        st = np.asarray(static_i[L.STATIC_I.index("SOILTYP")])
+        return np.lexsort((st, vt, np.asarray(isnow) < 0, band))
     raise ValueError(f"unknown column order key {key!r} (one of {KEYS})")
