@@ -42,6 +42,7 @@ import torch.distributed as dist
 from . import cases, layout as L, ncio, shard, timeman
 from .config import Config
 from .engine import ColumnState, Engine, StreamShards
+from .order import coherent_order
 from .params import Params
 
 
@@ -161,31 +162,50 @@ class OfflineDriver:
 
     @classmethod
     def from_files(cls, cfg: Config, device: int = 0, params: Params | None = None,
-                   init: str | None = None, **kw) -> "OfflineDriver":
+                   init: str | None = None, order: str | None = "lon-snow-type",
+                   **kw) -> "OfflineDriver":
         """The run the namelist describes: static file (cfg.constfile), initial
         state (cfg.initfile, or `init`) and LDASIN forcing (cfg.indir every
-        cfg.input_frequency), netCDF-3 files in the layouts of ncio.py."""
+        cfg.input_frequency), netCDF-3 files in the layouts of ncio.py.
+
+        order: the land points are laid out in the engine in this coherent
+        order (order.coherent_order; None = grid order).  The permutation is
+        applied when columns are read from the files and undone when they are
+        written, so files always hold the grid."""
         P = params or Params.builtin()
         grid, sf, si = ncio.read_static(cfg.constfile, P.as_dict(), cfg.begdatetime)
         st, isn, t0, step = ncio.read_state(init or cfg.initfile, grid)
-        sl = slice(0, grid.n)
-        if dist.is_initialized():  # this rank's block of the land points
+        perm = np.arange(grid.n) if order is None else coherent_order(grid.lon_rad, si, isn,
+                                                                      order, band_deg=4.0)
+        idx = perm
+        if dist.is_initialized():  # this rank's block of the (ordered) land points
             s0, cnt = shard.shard_range(grid.n, dist.get_rank(), dist.get_world_size())
-            sl = slice(s0, s0 + cnt)
-        cols = cases.ColumnSet(sf[:, sl], si[:, sl], st[:, sl], isn[sl], grid.lon_rad[sl],
+            idx = perm[s0:s0 + cnt]
+        cols = cases.ColumnSet(sf[:, idx], si[:, idx], st[:, idx], isn[idx], grid.lon_rad[idx],
                                *([None] * 6))
         forcing = ncio.LdasinForcing(cfg.indir, grid, cfg.begdatetime, cfg.input_interval,
-                                     cols=sl)
+                                     cols=idx)
         drv = cls(cfg, cols, device, P, forcing, grid=grid, **kw)
         drv.t, drv.step_index = t0, step
+        drv.perm, drv.cols_index = perm, idx
         return drv
+
+    def to_grid_order(self, a: np.ndarray) -> np.ndarray:
+        """(..., n) columns of the whole set in engine order -> land-point order."""
+        perm = getattr(self, "perm", None)
+        if perm is None:
+            return a
+        out = np.empty_like(a)
+        out[..., perm] = a
+        return out
 
     # ---- restart -----------------------------------------------------------------
     def save_restart(self, path: str):
         self.ranges.join()
         if path.endswith(".nc"):
-            ncio.write_state(path, self.grid, self.cs.state.cpu().numpy(),
-                             self.cs.isnow.cpu().numpy(), self.t, self.step_index)
+            ncio.write_state(path, self.grid, self.to_grid_order(self.cs.state.cpu().numpy()),
+                             self.to_grid_order(self.cs.isnow.cpu().numpy()), self.t,
+                             self.step_index)
             return
         np.savez(path, time=np.array(self.t.isoformat()), step=np.int64(self.step_index),
                  state=self.cs.state.cpu().numpy(), isnow=self.cs.isnow.cpu().numpy(),
@@ -198,8 +218,10 @@ class OfflineDriver:
         if path.endswith(".nc"):
             st, isn, self.t, self.step_index = ncio.read_state(path, self.grid,
                                                                self.cs.state.cpu().numpy().dtype)
-            self.cs.state.copy_(torch.as_tensor(st, device=self.dev))
-            self.cs.isnow.copy_(torch.as_tensor(isn, device=self.dev))
+            idx = getattr(self, "cols_index", slice(None))
+            self.cs.state.copy_(torch.as_tensor(np.ascontiguousarray(st[:, idx]),
+                                                device=self.dev))
+            self.cs.isnow.copy_(torch.as_tensor(np.ascontiguousarray(isn[idx]), device=self.dev))
             return
         with np.load(path, allow_pickle=False) as z:
             assert str(z["layout"]) == ",".join(n for n, _ in L.STATE_FIELDS), "state layout"
@@ -244,7 +266,8 @@ class OfflineDriver:
                     os.makedirs(cfg.outdir, exist_ok=True)
                     if self.grid is not None:
                         path = ncio.ldasout_path(cfg.outdir, t1)
-                        ncio.write_ldasout(path, self.grid, d.cpu().numpy(), t1)
+                        ncio.write_ldasout(path, self.grid, self.to_grid_order(d.cpu().numpy()),
+                                           t1)
                     else:
                         path = os.path.join(cfg.outdir, f"{_stamp(t1)}.LDASOUT.npz")
                         np.savez(path, time=np.array(t1.isoformat()),

@@ -278,7 +278,8 @@ class LdasinForcing:
 
     def __init__(self, indir: str, grid: Grid, begin: datetime.datetime,
                  every: datetime.timedelta, cols: slice | None = None):
-        """cols: the land-point block this rank steps (default: all of them)."""
+        """cols: the land points this rank steps, in engine order (a slice or an
+        index array; default: all of them in grid order)."""
         self.indir, self.grid, self.begin, self.every = indir, grid, begin, every
         self.cols = cols if cols is not None else slice(0, grid.n)
         self._t, self._fields = None, None

@@ -89,3 +89,26 @@ def test_frequencies_and_boundaries():
     assert driver._is_boundary(datetime.datetime(2000, 2, 1), t0, "1month")
     assert not driver._is_boundary(datetime.datetime(2000, 2, 1, 0, 15), t0, "1month")
     assert not driver._is_boundary(t0, t0, "1month")
+
+
+def test_coherent_order_is_a_permutation_grouping_keys():
+    """order.coherent_order: a permutation; within a longitude band the
+    snow-free and snow-covered columns, and the vegetation types, are grouped."""
+    import numpy as np
+    from noahmp_amd import cases, layout as L
+    from noahmp_amd.order import KEYS, coherent_order
+    from noahmp_amd.params import Params
+    cols = cases.make_columns(5000, "mixed", Params.builtin().as_dict(), seed=8)
+    for key in KEYS:
+        p = coherent_order(cols.lon, cols.static_i, cols.isnow, key)
+        assert np.array_equal(np.sort(p), np.arange(5000))
+    p = coherent_order(cols.lon, cols.static_i, cols.isnow, "lon-snow-type", band_deg=4.0)
+    band = np.floor(np.degrees(cols.lon[p]) / 4.0)
+    assert (np.diff(band) >= 0).all()
+    snow = (cols.isnow[p] < 0).astype(int)
+    vt = cols.static_i[L.STATIC_I.index("VEGTYP")][p]
+    for b in np.unique(band)[:5]:
+        m = band == b
+        assert (np.diff(snow[m]) >= 0).all()
+        for sv in (0, 1):
+            assert (np.diff(vt[m][snow[m] == sv]) >= 0).all()

@@ -81,9 +81,10 @@ def test_driver_from_netcdf_files(engine_lib, tmp_path):
     for k, t in enumerate([cfg.begdatetime + i * cfg.timestep for i in range(96)]):
         ncio.write_ldasin(ncio.ldasin_path(str(indir), t), grid, g["forcing"][k], t)
     drv = driver.OfflineDriver.from_files(cfg)
+    assert not np.array_equal(drv.perm, np.arange(32))  # the coherent order is a real permutation
     drv.run()
     assert drv.step_index == 96
-    assert bit_equal(drv.cs.state.cpu().numpy(), g["states"][-1]).all()
+    assert bit_equal(drv.to_grid_order(drv.cs.state.cpu().numpy()), g["states"][-1]).all()
     files = sorted(glob.glob(os.path.join(cfg.outdir, "*.LDASOUT_DOMAIN1")))
     assert len(files) == 8
     d = ncio.read_ldasout(files[-1], grid)
@@ -97,7 +98,10 @@ def test_driver_from_netcdf_files(engine_lib, tmp_path):
     b = driver.OfflineDriver.from_files(cfg, init=path, write=False)
     assert b.step_index == 40
     b.run()
-    assert bit_equal(b.cs.state.cpu().numpy(), g["states"][-1]).all()
+    assert bit_equal(b.to_grid_order(b.cs.state.cpu().numpy()), g["states"][-1]).all()
+    # grid order (order=None) gives the same bits
+    c = driver.OfflineDriver.from_files(cfg, init=path, write=False, order=None).run()
+    assert bit_equal(c.cs.state.cpu().numpy(), g["states"][-1]).all()
 
 
 def test_offline_cli_runs_a_netcdf_case(engine_lib, tmp_path):
@@ -161,7 +165,7 @@ def _driver_rank(rank, world, port, nml, out_dir):
     drv = driver.OfflineDriver.from_files(cfg)
     drv.run()
     np.savez(os.path.join(out_dir, f"rank{rank}.npz"), state=drv.cs.state.cpu().numpy(),
-             isnow=drv.cs.isnow.cpu().numpy())
+             isnow=drv.cs.isnow.cpu().numpy(), cols=drv.cols_index)
     dist.barrier()
     drv.engine.close()
     dist.destroy_process_group()
@@ -170,9 +174,9 @@ def _driver_rank(rank, world, port, nml, out_dir):
 @pytest.mark.parametrize("world", [2, 3])
 def test_driver_multi_rank_files_equal_reference(engine_lib, tmp_path, world):
     """OfflineDriver.from_files under a process group: each rank reads and
-    steps only its shard_range block of the 32 land points (ragged at world 3:
-    11/11/10), rank 0 gathers (shard.DiagGather) and writes LDASOUT for the
-    whole grid.  Every LDASOUT file and every rank's final state equal the
+    steps only its shard_range block of the 32 land points in the driver's
+    coherent column order (ragged at world 3: 11/11/10), rank 0 gathers
+    (shard.DiagGather) and writes LDASOUT for the whole grid in grid order.  Every LDASOUT file and every rank's final state equal the
     reference trajectory bit for bit."""
     import socket
     import torch.multiprocessing as mp
@@ -193,9 +197,13 @@ def test_driver_multi_rank_files_equal_reference(engine_lib, tmp_path, world):
         for i, name in enumerate(L.DIAG_OUT):
             if name != "T2M":
                 assert bit_equal(d[i], g["diags"][k][L.DIAG_FULL.index(name)]).all(), (fn, name)
+    seen = []
     for r in range(world):
         s0, cnt = shard.shard_range(32, r, world)
         with np.load(tmp_path / f"rank{r}.npz") as z:
-            assert z["state"].shape[1] == cnt
-            assert bit_equal(z["state"], g["states"][-1][:, s0:s0 + cnt]).all(), r
-            assert np.array_equal(z["isnow"], g["isnows"][-1][s0:s0 + cnt])
+            idx = z["cols"]  # this rank's land points, in the driver's coherent order
+            assert z["state"].shape[1] == cnt == idx.size
+            assert bit_equal(z["state"], g["states"][-1][:, idx]).all(), r
+            assert np.array_equal(z["isnow"], g["isnows"][-1][idx])
+            seen.append(idx)
+    assert np.array_equal(np.sort(np.concatenate(seen)), np.arange(32))
