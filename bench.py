@@ -259,6 +259,7 @@ def main():
                     tj.get("streams", 1) == len(ranges.ranges) and \
                     tj.get("math") == a.math and tj.get("kind", "mixed") == a.kind and \
                     tj.get("order", "as-generated") == a.order and \
+                    (a.order == "as-generated" or tj.get("order_band", 4.0) == a.order_band) and \
                     tj.get("out_every", 2) == a.out_every and \
                     tj.get("source_hash") == _build.source_hash() \
                     and os.environ.get("NOAHMP_ENGINE_LIB") is None:

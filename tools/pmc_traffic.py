@@ -59,6 +59,9 @@ def main():
     kind = "mixed"
     if "--kind" in sys.argv:
         kind = sys.argv[sys.argv.index("--kind") + 1]
+    order = "lon-snow-type"
+    if "--order" in sys.argv:
+        order = sys.argv[sys.argv.index("--order") + 1]
     cols_per_launch = ncol / streams
     calib_n, nf = 4194304, 56
     cal_bytes = nf * calib_n * 4
@@ -74,7 +77,7 @@ def main():
     import noahmp_pkg  # noqa: F401
     from noahmp_amd import build
     res = {"source_hash": build.source_hash(), "ncol": ncol, "streams": streams, "kind": kind,
-           "out_every": out_every,
+           "out_every": out_every, "order": order,
            "precision": 4, "math": "ref", "kernel": KERNEL, "dispatches": nb,
            "fetch_size_kb": bf, "write_size_kb": bw, "read_correction": rf,
            "write_correction": rw, "read_bytes": rd, "write_bytes": wr,
