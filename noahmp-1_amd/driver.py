@@ -10,6 +10,8 @@ offline/noahmp_config.py has no time loop, forcing reader or writer, SURVEY
 * forcing comes from a provider `forcing(step, t) -> (12, n)` array; the
   reference's LDASIN files are not in the repository, so `SyntheticForcing`
   (the seeded diurnal generator the tests and bench use) is the default;
+  `forcing="device"` generates the synthetic forcing on the GPU instead
+  (`DeviceSyntheticForcing`, nmp_forcing_synth);
 * output steps (Config.output_frequency) write the 16 surface fluxes as
   ``<outdir>/<YYYYMMDDHH>.LDASOUT_DOMAIN1`` (netCDF-3 on the grid, ncio.py)
   when the columns come from a grid, else ``<outdir>/<YYYYMMDDHH>.LDASOUT.npz``;
@@ -102,6 +104,18 @@ class ForcingUpload:
         self.consumed[self._last] = tuple(evs)
 
 
+class DeviceSyntheticForcing:
+    """Synthetic forcing generated on the device each step (nmp_forcing_synth):
+    no host generation, no upload -- the long-run path for synthetic cases
+    (a year of hourly forcing for 1 M columns would be 0.4-0.8 TB from the
+    host).  climate: (NCLIM, n) records of this rank's columns
+    (cases.climate); first_col: their global index (stateless draws)."""
+    on_device = True
+
+    def __init__(self, climate: np.ndarray, seed: int = 0, first_col: int = 0):
+        self.climate, self.seed, self.first_col = climate, seed, first_col
+
+
 def _stamp(t: datetime.datetime) -> str:
     return t.strftime("%Y%m%d%H")
 
@@ -142,7 +156,16 @@ class OfflineDriver:
         self.cs = ColumnState.from_host(cols, self.dev, self.dtype)
         # column ranges on their own streams: launch tails overlap (engine.StreamShards)
         self.ranges = StreamShards(self.engine, self.cs, streams)
+        if forcing == "device":
+            forcing = DeviceSyntheticForcing(cases.climate(cols), seed=0)
         self.forcing = forcing or SyntheticForcing(cols)
+        self.dev_forcing = None
+        if getattr(self.forcing, "on_device", False):
+            # two device buffers: step k writes buffer k % 2 on each range's
+            # stream right before that range's launch (stream order: reuse safe)
+            self.dev_forcing = (
+                torch.as_tensor(self.forcing.climate, device=self.dev).to(self.dtype).contiguous(),
+                torch.empty((2, L.NFORCING, self.cs.ncol), dtype=self.dtype, device=self.dev))
         self.zsoil = [float(z) for z in zsoil]
         self.dt = cfg.timestep.total_seconds()
         self.t = cfg.begdatetime
@@ -243,7 +266,17 @@ class OfflineDriver:
             t0 = self.t
             t1 = t0 + cfg.timestep
             out = _is_boundary(t1, cfg.begdatetime, out_every) and self.write
-            f = self.upload.put(self.forcing(self.step_index, t0))
+            pre, after = None, self.upload.stream
+            if self.dev_forcing is not None:
+                clim, fbuf = self.dev_forcing
+                f = fbuf[self.step_index % 2]
+                jul, yl, k = timeman.julian(t0), timeman.yearlen(t0.year), self.step_index
+                pre = lambda st, rng: self.engine.forcing_synth(  # noqa: E731
+                    clim, jul, yl, self.forcing.seed, k, f, self.forcing.first_col, stream=st,
+                    cols=rng)
+                after = torch.cuda.current_stream(self.dev)
+            else:
+                f = self.upload.put(self.forcing(self.step_index, t0))
             diag = self.diag
             if out and self.gather is not None:
                 b = self.n_out % len(self.gather.bufs)
@@ -251,8 +284,9 @@ class OfflineDriver:
                 diag = self.gather.local(b)
             self.ranges.step(f, self.zsoil, self.dt, timeman.julian(t0), timeman.yearlen(t0.year),
                              diag if out else None, L.DIAG_OUT_LEVEL if out else L.DIAG_NONE,
-                             after=self.upload.stream)
-            self.upload.consumed_by(self.ranges.streams)
+                             after=after, pre=pre)
+            if self.dev_forcing is None:
+                self.upload.consumed_by(self.ranges.streams)
             self.t, self.step_index = t1, self.step_index + 1
             if out:
                 if self.gather is not None:

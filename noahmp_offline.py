@@ -39,6 +39,9 @@ def main(argv=None):
     ap.add_argument("--kind", default="casenml", choices=("casenml", "mixed", "conus", "global"))
     ap.add_argument("--device", type=int, default=0)
     ap.add_argument("--restart", default=None, help="restart file to start from")
+    ap.add_argument("--device-forcing", action="store_true",
+                    help="synthetic cases: generate the forcing on the GPU every step "
+                         "(nmp_forcing_synth) instead of on the host")
     a = ap.parse_args(argv)
     cfg = config.Config(a.nmlfile)
     P = Params.builtin()
@@ -48,7 +51,8 @@ def main(argv=None):
     else:
         cols = cases.make_columns(a.ncol, a.kind, P.as_dict(), seed=0,
                                   julian=timeman.julian(cfg.begdatetime))
-        drv = driver.OfflineDriver(cfg, cols, device=a.device, params=P)
+        drv = driver.OfflineDriver(cfg, cols, device=a.device, params=P,
+                                   forcing="device" if a.device_forcing else None)
         if a.restart:
             drv.load_restart(a.restart)
     t0 = time.perf_counter()

@@ -207,3 +207,36 @@ def test_driver_multi_rank_files_equal_reference(engine_lib, tmp_path, world):
             assert np.array_equal(z["isnow"], g["isnows"][-1][idx])
             seen.append(idx)
     assert np.array_equal(np.sort(np.concatenate(seen)), np.arange(32))
+
+
+def test_driver_device_forcing_equals_engine_steps(engine_lib, tmp_path):
+    """OfflineDriver(forcing="device"): each step's forcing generated on the
+    device per range (nmp_forcing_synth on the range streams) gives the same
+    bits as generating the whole step's forcing in one launch and stepping the
+    engine directly."""
+    from noahmp_amd.engine import ColumnState, Engine
+    from noahmp_amd.params import Params
+    cfg = _cfg(tmp_path)
+    cols = cases.make_columns(50_001, "mixed", Params.builtin().as_dict(), seed=12,
+                              julian=timeman_julian(cfg))
+    drv = driver.OfflineDriver(cfg, cols, forcing="device", write=False).run(nsteps=10)
+    eng = Engine(Params.builtin(), cfg.engine_options(), device=0)
+    cs = ColumnState.from_host(cols, "cuda:0")
+    clim = torch.as_tensor(cases.climate(cols, np.float32), device="cuda:0")
+    f = torch.empty((L.NFORCING, cols.n), device="cuda:0")
+    from noahmp_amd import timeman
+    t = cfg.begdatetime
+    for k in range(10):
+        eng.forcing_synth(clim, timeman.julian(t), timeman.yearlen(t.year), 0, k, f)
+        eng.step(cs, f, cases.CASE_NML_ZSOIL, cfg.timestep.total_seconds(), timeman.julian(t),
+                 timeman.yearlen(t.year))
+        t = t + cfg.timestep
+    torch.cuda.synchronize()
+    assert torch.equal(drv.cs.state.view(torch.int32), cs.state.view(torch.int32))
+    assert torch.equal(drv.cs.isnow, cs.isnow)
+    eng.close()
+
+
+def timeman_julian(cfg):
+    from noahmp_amd import timeman
+    return timeman.julian(cfg.begdatetime)
