@@ -20,6 +20,8 @@
 //    mask; wave-uniform option branches become scalar branches.
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "dev_params.h"
 #include "sflx_kargs.h"
 #include "sflx_math.h"
@@ -1205,6 +1207,89 @@ DEV void sflx_column(const DevParams& P, const KArgs<T>& A, Col<T>& c, const Sin
         (o.sfc == 1) ? Sfc1Logs<T, R>(zlvl, zpd, z0m, z0h, c.status,
                                       (sizeof(T) == 4 && R) ? &log_2z0m_v : nullptr)
                      : Sfc1Logs<T, R>{};
+#ifndef NMP_VEGE_NOPEEL
+    // One Newton iteration (loop1, func.f90:2744-2877).  Iteration 1 is peeled
+    // (it alone calls stomata/canres, :2779-2803), so the loop that runs the
+    // remaining iterations carries none of stomata's code or registers.
+    auto vege_iter = [&](const int iter, auto first) -> T {
+        if (o.sfc == 1)
+          sfcdif1<T, R>(iter, c.sfctmp, rhoair, h, qair, zlvl, zpd, lgv, z0h, ur, mpe, moz, mozsgn,
+                        fm, fh, fm2, fh2, cmv, chv, fv);
+        if (o.sfc == 2) {
+          sfcdif2<T, R>(iter, z0m, c.tah, thair, ur, (T)P.g.czil, zlvl, cmv, chv, moz, wstar, fv);
+          chv = chv / ur;
+          cmv = cmv / ur;
+        }
+        rahc = rmax(L(1.0), L(1.0) / (chv * ur));
+        T rawc = rahc;
+        ragrb<T, R>(sqrt_dleaf_uc, iter, vaie, rhoair, hg, c.tah, zpd, z0mg, z0mg, hcan, z0h, fv,
+                    cwp, mpe, fhg, rahg, rb);
+        T rawg = rahg;
+        tt = tdc(c.tv);
+        T estv, destv;
+        esat_sel(tt, estv, destv);
+        if constexpr (decltype(first)::value) {  // iter == 1
+          if (o.crs == 1) {
+            const StomataPre<T> sp =
+                stomata_pre<T, R>(V, parsun > L(0.0) || parsha > L(0.0), c.sfcprs, c.sfctmp, c.tv,
+                                  c.o2air, c.foln, btran, rb);
+            stomata_solve<T, R>(V, sp, igs, c.sfcprs, parsun, c.eah, estv, c.co2air, rssun, psnsun);
+            stomata_solve<T, R>(V, sp, igs, c.sfcprs, parsha, c.eah, estv, c.co2air, rssha, psnsha);
+          }
+          if (o.crs == 2) {
+            canres<T, R>(V, c.sfcprs, c.tv, parsun, c.eah, btran, rssun, psnsun);
+            canres<T, R>(V, c.sfcprs, c.tv, parsha, c.eah, btran, rssha, psnsha);
+          }
+        }
+        cah = L(1.0) / rahc;
+        cvh = L(2.0) * vaie / rb;
+        T cgh = L(1.0) / rahg;
+        T cond = cah + cvh + cgh;
+        T ata = (c.sfctmp * cah + tgv * cgh) / cond;
+        T bta = cvh / cond;
+        T csh = (L(1.0) - bta) * rhoair * CPAIR * cvh;
+        T caw = L(1.0) / rawc;
+        T cew = c.fwet * vaie / rb;
+        T ctw = (L(1.0) - c.fwet) * (laisune / (rb + rssun) + laishae / (rb + rssha));
+        T cgw = L(1.0) / (rawg + rsurf);
+        cond = caw + cew + ctw + cgw;
+        T aea = (eair * caw + estg * cgw) / cond;
+        T bea = (cew + ctw) / cond;
+        T cev = (L(1.0) - bea) * cew * rhoair * CPAIR / gammav;
+        T ctr = (L(1.0) - bea) * ctw * rhoair * CPAIR / gammav;
+        c.tah = ata + bta * c.tv;
+        c.eah = aea + bea * estv;
+        irc = fveg * (air + cir * p4(c.tv));
+        shc = fveg * rhoair * CPAIR * cvh * (c.tv - c.tah);
+        evc = fveg * rhoair * CPAIR * cew * (estv - c.eah) / gammav;
+        tr = fveg * rhoair * CPAIR * ctw * (estv - c.eah) / gammav;
+        if (c.tv > TFRZ)
+          evc = rmin(c.canliq * latheav / DT, evc);
+        else
+          evc = rmin(c.canice * latheav / DT, evc);
+        T b = sav - irc - shc - evc - tr;
+        T a = fveg * (L(4.0) * cir * p3(c.tv) + csh + (cev + ctr) * destv);
+        T dtv = b / a;
+        irc = irc + fveg * L(4.0) * cir * p3(c.tv) * dtv;
+        shc = shc + fveg * csh * dtv;
+        evc = evc + fveg * cev * destv * dtv;
+        tr = tr + fveg * ctr * destv * dtv;
+        c.tv = c.tv + dtv;
+        h = rhoair * CPAIR * (c.tah - c.sfctmp) / rahc;
+        hg = rhoair * CPAIR * (tgv - c.tah) / rahg;
+        c.qsfc = (L(0.622) * c.eah) / (c.sfcprs - L(0.378) * c.eah);
+        return dtv;
+    };
+    vtrips = 1;
+    vege_iter(1, std::true_type{});  // iter 1 cannot exit (the test needs iter >= 5)
+#pragma unroll 1
+    for (int iter = 2; iter <= 20; ++iter) {
+      vtrips = iter;
+      const T dtv = vege_iter(iter, std::false_type{});
+      if (liter == 1) break;
+      if (iter >= 5 && fabs(dtv) <= L(0.01) && liter == 0) liter = 1;
+    }
+#else
 #pragma unroll 1
     for (int iter = 1; iter <= 20; ++iter) {
       vtrips = iter;
@@ -1277,6 +1362,7 @@ DEV void sflx_column(const DevParams& P, const KArgs<T>& A, Col<T>& c, const Sin
       if (liter == 1) break;
       if (iter >= 5 && fabs(dtv) <= L(0.01) && liter == 0) liter = 1;
     }
+#endif
     // under-canopy fluxes and TG (loop2, :2881-2914)
     air = -emg * (L(1.0) - emv) * c.lwdn - emg * emv * SB * p4(c.tv);
     cir = emg * SB;

@@ -58,6 +58,7 @@ VARIANTS = {
     # timing probes only (NOT bit-exact): upper bounds of what faster division
     # / sqrt sequences could save
     "nocrdiv": ("-fno-hip-fp32-correctly-rounded-divide-sqrt",),
+    "nopeel": ("-DNMP_VEGE_NOPEEL",),
 }
 if __name__ == "__main__":
     names = sys.argv[1:] or list(VARIANTS)
