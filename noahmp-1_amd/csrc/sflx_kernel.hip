@@ -1212,6 +1212,7 @@ DEV void sflx_column(const DevParams& P, const KArgs<T>& A, Col<T>& c, const Sin
     // (it alone calls stomata/canres, :2779-2803), so the loop that runs the
     // remaining iterations carries none of stomata's code or registers.
     auto vege_iter = [&](const int iter, auto first) -> T {
+      if constexpr (!decltype(first)::value) __builtin_assume(iter >= 2);
         if (o.sfc == 1)
           sfcdif1<T, R>(iter, c.sfctmp, rhoair, h, qair, zlvl, zpd, lgv, z0h, ur, mpe, moz, mozsgn,
                         fm, fh, fm2, fh2, cmv, chv, fv);
