@@ -25,6 +25,7 @@ struct nmp_engine {
   int math;  // 0 = reference-rounded transcendentals (parity), 1 = fast (fp32 only)
   int cpw;   // columns per wave: 8..64, or 0 = chosen per launch from ncol
   int simds; // SIMDs on the device (CUs x 4)
+  int os;    // compiled option set matching opts (sflx_kernel.hip kOptionSet), 0 = none
   nmp_options opts;
   nmp::DevParams* dparams;
 };
@@ -39,6 +40,16 @@ bool options_ok(const nmp_options& o) {
          o.opt_inf >= 1 && o.opt_inf <= 2 && o.opt_rad >= 1 && o.opt_rad <= 3 &&
          o.opt_alb >= 1 && o.opt_alb <= 2 && o.opt_snf >= 1 && o.opt_snf <= 3 &&
          o.opt_tbot >= 1 && o.opt_tbot <= 2 && o.opt_stc >= 1 && o.opt_stc <= 2;
+}
+
+// the kernel's compiled option sets (sflx_kernel.hip kOptionSet): 1 =
+// run/case.nml's options, 2 = the same with opt_veg = 2; 0 = none matches
+int option_set(const nmp_options& o) {
+  const bool rest = o.opt_crs == 1 && o.opt_btr == 1 && o.opt_run == 1 && o.opt_sfc == 1 &&
+                    o.opt_frz == 1 && o.opt_inf == 1 && o.opt_rad == 1 && o.opt_alb == 2 &&
+                    o.opt_snf == 1 && o.opt_tbot == 1 && o.opt_stc == 1;
+  if (!rest) return 0;
+  return o.opt_veg == 1 ? 1 : o.opt_veg == 2 ? 2 : 0;
 }
 
 int ensure_device(int dev) {
@@ -106,13 +117,13 @@ int launch(const nmp_engine* e, int64_t ncol, int64_t ld, const float zsoil[4], 
     fill_args(a, e, ncol, ld, zsoil, dt, julian, yearlen, state, isnow, sf, si, fc, diag,
               diag_level, status, order, cost, ficeold);
     const bool small = small_launch(e, ncol);
-    err = (e->math == 0) ? nmp::launch_sflx<float, true>(e->dparams, a, stream, small)
-                         : nmp::launch_sflx<float, false>(e->dparams, a, stream, small);
+    err = (e->math == 0) ? nmp::launch_sflx<float, true>(e->dparams, a, stream, small, e->os)
+                         : nmp::launch_sflx<float, false>(e->dparams, a, stream, small, 0);
   } else {
     nmp::KArgs<double> a;
     fill_args(a, e, ncol, ld, zsoil, dt, julian, yearlen, state, isnow, sf, si, fc, diag,
               diag_level, status, order, cost, ficeold);
-    err = nmp::launch_sflx<double, false>(e->dparams, a, stream, small_launch(e, ncol));
+    err = nmp::launch_sflx<double, false>(e->dparams, a, stream, small_launch(e, ncol), e->os);
   }
   return err == hipSuccess ? NMP_OK : NMP_E_DEVICE;
 }
@@ -189,6 +200,9 @@ int nmp_init(const nmp_params* params, const nmp_options* opts, int device, int 
     ncu = 256;
   e->simds = 4 * ncu;
   e->opts = *opts;
+  // NMP_GENERIC_OPTIONS=1: always the run-time-options kernel (A/B tests, timing)
+  const char* g = std::getenv("NMP_GENERIC_OPTIONS");
+  e->os = (g && std::strcmp(g, "1") == 0) ? 0 : option_set(*opts);
   e->dparams = d;
   *out = e;
   return NMP_OK;

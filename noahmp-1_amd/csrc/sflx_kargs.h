@@ -51,7 +51,7 @@ struct KArgs {
 
 template <class T, bool R>
 hipError_t launch_sflx(const DevParams* dparams, const KArgs<T>& a, hipStream_t stream,
-                       bool small);
+                       bool small, int os);
 
 // csrc/forcing.hip: synthetic forcing of one step from the climate records
 hipError_t launch_forcing_synth(int precision, int64_t ncol, int64_t ld, const void* clim,

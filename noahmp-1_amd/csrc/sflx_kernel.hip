@@ -828,13 +828,23 @@ struct PhaseClock {
 #define NMP_PHASE(i) ((void)0)
 #endif
 
-template <class T, bool R>
+// Option sets compiled as constants (kernel template parameter OS): with the
+// options known at compile time every `if (o.xxx == k)` of the other values
+// folds away, which shortens the code and the live ranges of the hot loops.
+// OS 0 reads the launch's options (every combination); 1 is run/case.nml's set
+// (configs #1-#4), 2 the same with dynamic vegetation + carbon (opt_veg = 2,
+// config #5).  The engine picks the set that matches its options.
+constexpr Opt kOptionSet[3] = {{1, 1, 1, 1, 1, 1, 1, 1, 2, 1, 1, 1},
+                               {1, 1, 1, 1, 1, 1, 1, 1, 2, 1, 1, 1},
+                               {2, 1, 1, 1, 1, 1, 1, 1, 2, 1, 1, 1}};
+
+template <class T, bool R, int OS>
 DEV void sflx_column(const DevParams& P, const KArgs<T>& A, Col<T>& c, const Sink<T>& out) {
   typedef Mth<T, R> M;
 #ifdef NMP_PHASE_TIMING
   PhaseClock pclk{__builtin_amdgcn_s_memtime(), 0};
 #endif
-  const Opt& o = A.o;
+  const Opt o = OS == 0 ? A.o : kOptionSet[OS];
   const VegRec& V = P.veg[c.lutyp - 1];
   const SoilRec& S = P.soil[c.sltyp - 1];
   const T DT = (T)A.dt;
@@ -2701,7 +2711,7 @@ constexpr int waves_per_eu(bool small) {
   return sizeof(T) == 4 ? (small ? NMP_WAVES_PER_EU / 2 : NMP_WAVES_PER_EU)
                         : (small ? (NMP_WAVES_PER_EU_F64 + 1) / 2 : NMP_WAVES_PER_EU_F64);
 }
-template <class T, bool R, bool SMALL>
+template <class T, bool R, bool SMALL, int OS>
 __global__ __launch_bounds__(NMP_BLOCK)
 __attribute__((amdgpu_waves_per_eu(waves_per_eu<T>(SMALL))))
 void sflx_step_kernel(const DevParams* __restrict__ gparams,
@@ -2776,26 +2786,42 @@ void sflx_step_kernel(const DevParams* __restrict__ gparams,
   const Sink<T> out{a.diag ? a.diag + c0 : nullptr, a.state + c0, ld, a.diag_level, sf, si, fc,
                     a.isnow + c0, a.cost ? a.cost + c0 : nullptr,
                     a.ficeold ? a.ficeold + c0 : nullptr};
-  sflx_column<T, R>(sp, a, c, out);
+  sflx_column<T, R, OS>(sp, a, c, out);
 
   if (c.status != 0) a.status[c0] |= c.status;
 }
 
 // launch wrapper (one instantiation per precision / math policy)
+template <class T, bool R, bool SMALL>
+void launch_os(int os, dim3 grid, dim3 block, hipStream_t stream, const DevParams* dparams,
+               const KArgs<T>& a) {
+  if (os == 1)
+    hipLaunchKernelGGL((sflx_step_kernel<T, R, SMALL, 1>), grid, block, 0, stream, dparams, a);
+  else if (os == 2)
+    hipLaunchKernelGGL((sflx_step_kernel<T, R, SMALL, 2>), grid, block, 0, stream, dparams, a);
+  else
+    hipLaunchKernelGGL((sflx_step_kernel<T, R, SMALL, 0>), grid, block, 0, stream, dparams, a);
+}
+
+// launch wrapper (one instantiation per precision / math policy).  os: the
+// compiled option set matching the engine's options (0 = read at run time)
 template <class T, bool R>
 hipError_t launch_sflx(const DevParams* dparams, const KArgs<T>& a, hipStream_t stream,
-                       bool small) {
+                       bool small, int os) {
   const int64_t cols_per_block = (int64_t)(NMP_BLOCK / 64) * a.cpw;
   const int64_t grid = (a.ncol + cols_per_block - 1) / cols_per_block;
   const int block = NMP_BLOCK;
   if (grid == 0) return hipSuccess;
-  // the fast-math fp32 path has no small instantiation (code size)
-  if (small && (sizeof(T) == 8 || R))
-    hipLaunchKernelGGL((sflx_step_kernel<T, R, (sizeof(T) == 8 || R)>), dim3((unsigned)grid),
-                       dim3(block), 0, stream, dparams, a);
-  else
-    hipLaunchKernelGGL((sflx_step_kernel<T, R, false>), dim3((unsigned)grid), dim3(block), 0,
+  // the fast-math fp32 path has neither a small nor option-set instantiation (code size)
+  if constexpr (sizeof(T) == 8 || R) {
+    if (small)
+      launch_os<T, R, true>(os, dim3((unsigned)grid), dim3(block), stream, dparams, a);
+    else
+      launch_os<T, R, false>(os, dim3((unsigned)grid), dim3(block), stream, dparams, a);
+  } else {
+    hipLaunchKernelGGL((sflx_step_kernel<T, R, false, 0>), dim3((unsigned)grid), dim3(block), 0,
                        stream, dparams, a);
+  }
   return hipGetLastError();
 }
 
@@ -2812,10 +2838,10 @@ extern "C" int nmp_debug_phase_cycles(unsigned long long* out16, int reset) {
 }
 #endif
 template hipError_t launch_sflx<float, true>(const DevParams*, const KArgs<float>&, hipStream_t,
-                                             bool);
+                                             bool, int);
 template hipError_t launch_sflx<float, false>(const DevParams*, const KArgs<float>&, hipStream_t,
-                                              bool);
+                                              bool, int);
 template hipError_t launch_sflx<double, false>(const DevParams*, const KArgs<double>&, hipStream_t,
-                                               bool);
+                                               bool, int);
 
 }  // namespace nmp
