@@ -346,6 +346,16 @@ int nmp_set_math(nmp_engine* eng, int mode);
  * Results do not depend on it. */
 int nmp_set_cols_per_wave(nmp_engine* eng, int cpw);
 
+/* Kernel specialisation for the engine's physics options.  The kernel is
+ * compiled for fixed option sets (case.nml's, and case.nml with opt_veg 2);
+ * nmp_init picks the one equal to the engine's options, any other combination
+ * runs the run-time-options kernel (set 0).  request: -1 = query only,
+ * 0 = force the run-time-options kernel, 1 = pick the matching compiled set
+ * (the default; env NMP_GENERIC_OPTIONS=1 makes nmp_init start at 0).
+ * Returns the set in use (>= 0) or a negative NMP_E_* code.  Results do not
+ * depend on it (DESIGN.md "Compile-time option sets"). */
+int nmp_option_set(nmp_engine* eng, int request);
+
 int nmp_engine_info(const nmp_engine* eng, int* device, int* precision, nmp_options* opts);
 void nmp_finalize(nmp_engine* eng);
 const char* nmp_strerror(int code);

@@ -220,6 +220,13 @@ int nmp_set_cols_per_wave(nmp_engine* eng, int cpw) {
   return NMP_OK;
 }
 
+int nmp_option_set(nmp_engine* eng, int request) {
+  if (!eng || request < -1 || request > 1) return NMP_E_ARG;
+  if (request == 0) eng->os = 0;
+  if (request == 1) eng->os = option_set(eng->opts);
+  return eng->os;
+}
+
 int nmp_engine_info(const nmp_engine* eng, int* device, int* precision, nmp_options* opts) {
   if (!eng) return NMP_E_ARG;
   if (device) *device = eng->device;

@@ -86,6 +86,13 @@ class Engine:
         """nmp_set_cols_per_wave: 8..64 columns per wave, 0 = 64 (default)."""
         _lib.check(self._lib.nmp_set_cols_per_wave(self._h, int(cpw)), "nmp_set_cols_per_wave")
 
+    def option_set(self, request: int = -1) -> int:
+        """nmp_option_set: the compiled option set the kernel runs (0 = the
+        run-time-options kernel); request 0 forces set 0, 1 picks the match."""
+        rc = self._lib.nmp_option_set(self._h, int(request))
+        _lib.check(min(rc, 0), "nmp_option_set")
+        return rc
+
     def set_math(self, mode: int):
         _lib.check(self._lib.nmp_set_math(self._h, int(mode)), "nmp_set_math")
         self.math = int(mode)

@@ -397,6 +397,49 @@ def test_rebinned_steps_equal_plain_steps(engines, tile, every):
         assert (o != np.arange(hi - lo)).any()
 
 
+@pytest.mark.parametrize("opt_veg,precision", [(1, 4), (2, 4), (1, 8), (2, 8)])
+def test_option_set_kernels_equal_generic(opt_veg, precision):
+    """The compiled option-set kernels (case.nml options = set 1, + opt_veg 2
+    = set 2) == the run-time-options kernel (set 0), bitwise, over 4 steps of
+    120,001 mixed columns with output on alternate steps -- ragged, every
+    vegetation/soil type, snow, water and ice columns."""
+    from noahmp_amd.engine import ColumnState, Engine
+    from noahmp_amd.params import Params
+    n = 120_001
+    opts = dict(L.CASE_NML_OPTIONS, opt_veg=opt_veg)
+    tab = Params.builtin()
+    a_eng = Engine(tab, opts, device=0, precision=precision)
+    b_eng = Engine(tab, opts, device=0, precision=precision)
+    try:
+        assert a_eng.option_set() == opt_veg  # kOptionSet[1] / [2]
+        assert b_eng.option_set(0) == 0 and b_eng.option_set() == 0
+        dtype = torch.float32 if precision == 4 else torch.float64
+        cols = cases.make_columns(n, "mixed", tab.as_dict(), seed=11, julian=170.0)
+        F = [torch.as_tensor(cases.forcing_step(cols, 170.0 + s / 48.0, 365, s, seed=11),
+                             device=DEV).to(dtype) for s in range(4)]
+        a = ColumnState.from_host(cols, DEV, dtype)
+        b = ColumnState.from_host(cols, DEV, dtype)
+        for s in range(4):
+            lvl = L.DIAG_FULL_LEVEL if s % 2 else L.DIAG_NONE
+            da = torch.zeros((L.NDIAG_FULL, n), dtype=dtype, device=DEV) if s % 2 else None
+            db = torch.zeros((L.NDIAG_FULL, n), dtype=dtype, device=DEV) if s % 2 else None
+            for eng, cs, d in ((a_eng, a, da), (b_eng, b, db)):
+                eng.step(cs, F[s], cases.CASE_NML_ZSOIL, 1800.0, 170.0 + s / 48.0, 365, d, lvl)
+            torch.cuda.synchronize()
+            if d is not None:
+                assert torch.equal(da.view(torch.int8), db.view(torch.int8)), s
+        assert torch.equal(a.state.view(torch.int8), b.state.view(torch.int8))
+        assert torch.equal(a.isnow, b.isnow) and torch.equal(a.status, b.status)
+        # set 1 is picked back when asked; another option combination has no set
+        assert b_eng.option_set(1) == opt_veg
+    finally:
+        a_eng.close()
+        b_eng.close()
+    c_eng = Engine(tab, dict(opts, opt_run=2), device=0, precision=precision)
+    assert c_eng.option_set() == 0
+    c_eng.close()
+
+
 @pytest.mark.parametrize("cpw", [8, 24, 40, 64])
 def test_cols_per_wave_bit_identical(engines, cpw):
     """Columns per wave (nmp_set_cols_per_wave) only changes the lane -> column
