@@ -29,5 +29,5 @@ done
 [ "${PMC:-1}" = 1 ] || exit 0
 TAG=${TAG:-occ}_pmc VALU=1 bash tools/pmc_run.sh || exit 1
 cd /tmp && export TMPDIR=/tmp
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/$OUT/ktrace" -o run -- python3 "$GRAFT_REPO_ROOT/bench.py" --no-cpu-baseline > "$GRAFT_REPO_ROOT/$OUT/ktrace.log" 2>&1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$GRAFT_REPO_ROOT/$OUT/ktrace" -o run -- python3 "$GRAFT_REPO_ROOT/bench.py" --no-cpu-baseline > "$GRAFT_REPO_ROOT/$OUT/ktrace.log" 2>&1
 echo "ktrace rc=$?"
