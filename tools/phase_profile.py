@@ -28,6 +28,10 @@ def main():
     math = sys.argv[3] if len(sys.argv) > 3 else "ref"
     P = Params.builtin()
     cols = cases.make_columns(n, kind, P.as_dict(), seed=1000, julian=180.0)
+    order = sys.argv[4] if len(sys.argv) > 4 else "lon-snow-type"
+    if order != "as-generated":  # the bench's default column order
+        from noahmp_amd.order import coherent_order
+        cols = cols.take(coherent_order(cols.lon, cols.static_i, cols.isnow, order))
     eng = Engine(P, L.CASE_NML_OPTIONS, 0, 4, math)
     lib = eng._lib
     lib.nmp_debug_phase_cycles.argtypes = [C.c_void_p, C.c_int]
@@ -44,7 +48,7 @@ def main():
     lib.nmp_debug_phase_cycles(buf, 0)
     v = np.array(list(buf), dtype=np.float64)
     tot = v.sum()
-    print(f"ncol={n} kind={kind} math={math}: wave-cycles per column-step "
+    print(f"ncol={n} kind={kind} math={math} order={order}: wave-cycles per column-step "
           f"{tot / (8 * n / 64) / 64:.0f} (per lane-equivalent)")
     for i in np.argsort(-v):
         if v[i] > 0:
