@@ -251,12 +251,12 @@ DEV void sfcdif1(int iter, T sfctmp, T rhoair, T h, T qair, T zlvl, T zpd, const
   }
   T fmnew, fhnew, fm2new, fh2new;
   if (moz < L(0.0)) {
-    T tmp1 = M::pow(L(1.0) - L(16.0) * moz, L(0.25));
+    T tmp1 = M::pow_q(L(1.0) - L(16.0) * moz);
     T tmp2 = M::log((L(1.0) + tmp1 * tmp1) / L(2.0));
     T tmp3 = M::log((L(1.0) + tmp1) / L(2.0));
     fmnew = L(2.0) * tmp3 + tmp2 - L(2.0) * M::atan(tmp1) + L(1.5707963);
     fhnew = L(2.0) * tmp2;
-    T tmp12 = M::pow(L(1.0) - L(16.0) * moz2, L(0.25));
+    T tmp12 = M::pow_q(L(1.0) - L(16.0) * moz2);
     T tmp22 = M::log((L(1.0) + tmp12 * tmp12) / L(2.0));
     T tmp32 = M::log((L(1.0) + tmp12) / L(2.0));
     fm2new = L(2.0) * tmp32 + tmp22 - L(2.0) * M::atan(tmp12) + L(1.5707963);
@@ -384,7 +384,7 @@ DEV void ragrb(T sqrt_dleaf_uc, int iter, T vai, T rhoair, T hg, T tah, T zpd, T
     T molg = L(-1.) * p3(fv) / tmp1;
     mozg = rmin((zpd - z0mg) / molg, L(1.0));
   }
-  T fhgnew = (mozg < L(0.0)) ? M::pow(L(1.0) - L(15.0) * mozg, L(-0.25)) : L(1.0) + L(4.7) * mozg;
+  T fhgnew = (mozg < L(0.0)) ? M::pow_mq(L(1.0) - L(15.0) * mozg) : L(1.0) + L(4.7) * mozg;
   fhg = (iter == 1) ? fhgnew : L(0.5) * (fhg + fhgnew);
   T cwpc = M::sqrt(cwp * vai * hcan * fhg);
   T tmp1 = M::exp(-cwpc * z0hg / hcan);
@@ -827,6 +827,13 @@ struct PhaseClock {
 #else
 #define NMP_PHASE(i) ((void)0)
 #endif
+
+// Unroll factor of the vege_flux Newton loop (tuning knob, results identical).
+#ifndef NMP_VEGE_UNROLL
+#define NMP_VEGE_UNROLL 1
+#endif
+#define NMP_STR(x) #x
+#define NMP_UNROLL(n) _Pragma(NMP_STR(unroll n))
 
 // Option sets compiled as constants (kernel template parameter OS): with the
 // options known at compile time every `if (o.xxx == k)` of the other values
@@ -1293,7 +1300,7 @@ DEV void sflx_column(const DevParams& P, const KArgs<T>& A, Col<T>& c, const Sin
     };
     vtrips = 1;
     vege_iter(1, std::true_type{});  // iter 1 cannot exit (the test needs iter >= 5)
-#pragma unroll 1
+    NMP_UNROLL(NMP_VEGE_UNROLL)
     for (int iter = 2; iter <= 20; ++iter) {
       vtrips = iter;
       const T dtv = vege_iter(iter, std::false_type{});
@@ -1534,7 +1541,7 @@ DEV void sflx_column(const DevParams& P, const KArgs<T>& A, Col<T>& c, const Sin
   if (fire <= L(0.0)) c.status |= NMP_ST_FIRE;
   T emissi = fveg * (emg * (L(1.) - emv) + emv + emv * (L(1.) - emv) * (L(1.) - emg)) +
              (L(1.) - fveg) * emg;
-  T trad = M::pow((fire - (L(1.0) - emissi) * c.lwdn) / (emissi * SB), L(0.25));
+  T trad = M::pow_q((fire - (L(1.0) - emissi) * c.lwdn) / (emissi * SB));
   T apar = parsun * laisun + parsha * laisha;
   T psn = psnsun * laisun + psnsha * laisha;
   // error(): energy balance (func.f90:712-721), a function of final energy terms only

@@ -59,6 +59,9 @@ VARIANTS = {
     # / sqrt sequences could save
     "nocrdiv": ("-fno-hip-fp32-correctly-rounded-divide-sqrt",),
     "nopeel": ("-DNMP_VEGE_NOPEEL",),
+    "vu2": ("-DNMP_VEGE_UNROLL=2",),
+    "vu3": ("-DNMP_VEGE_UNROLL=3",),
+    "pinnv": ("-DNMP_PIN_NONVOLATILE",),
 }
 if __name__ == "__main__":
     names = sys.argv[1:] or list(VARIANTS)
