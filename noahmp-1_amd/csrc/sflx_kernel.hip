@@ -234,11 +234,11 @@ DEV void sfcdif1(int iter, T sfctmp, T rhoair, T h, T qair, T zlvl, T zpd, const
     moz2 = L(0.0);
   } else {
     T tvir = (L(1.0) + L(0.61) * qair) * sfctmp;
-    T tmp1 = KARMAN * (GRAV / tvir) * h / (rhoair * CPAIR);
+    T tmp1 = dv(KARMAN * dv(GRAV, tvir) * h, rhoair * CPAIR);
     if (fabs(tmp1) <= mpe) tmp1 = mpe;
-    T mol = L(-1.0) * p3(fv) / tmp1;
-    moz = rmin((zlvl - zpd) / mol, L(1.0));
-    moz2 = rmin((L(2.0) + z0h) / mol, L(1.0));
+    T mol = dv(L(-1.0) * p3(fv), tmp1);
+    moz = rmin(dv(zlvl - zpd, mol), L(1.0));
+    moz2 = rmin(dv(L(2.0) + z0h, mol), L(1.0));
   }
   if (mozold * moz < L(0.0)) mozsgn = mozsgn + 1;
   if (mozsgn >= 2) {
@@ -290,8 +290,8 @@ DEV void sfcdif1(int iter, T sfctmp, T rhoair, T h, T qair, T zlvl, T zpd, const
   if (fabs(chfh) <= mpe) chfh = mpe;
   if (fabs(cm2fm2) <= mpe) cm2fm2 = mpe;
   if (fabs(ch2fh2) <= mpe) ch2fh2 = mpe;
-  cm = KARMAN * KARMAN / (cmfm * cmfm);
-  ch = KARMAN * KARMAN / (cmfm * chfh);
+  cm = dv(KARMAN * KARMAN, cmfm * cmfm);
+  ch = dv(KARMAN * KARMAN, cmfm * chfh);
   fv = ur * M::sqrt(cm);
 }
 
@@ -379,20 +379,20 @@ DEV void ragrb(T sqrt_dleaf_uc, int iter, T vai, T rhoair, T hg, T tah, T zpd, T
   typedef Mth<T, R> M;
   T mozg = L(0.0);
   if (iter > 1) {
-    T tmp1 = KARMAN * (GRAV / tah) * hg / (rhoair * CPAIR);
+    T tmp1 = dv(KARMAN * dv(GRAV, tah) * hg, rhoair * CPAIR);
     if (fabs(tmp1) <= mpe) tmp1 = mpe;
-    T molg = L(-1.) * p3(fv) / tmp1;
-    mozg = rmin((zpd - z0mg) / molg, L(1.0));
+    T molg = dv(L(-1.) * p3(fv), tmp1);
+    mozg = rmin(dv(zpd - z0mg, molg), L(1.0));
   }
   T fhgnew = (mozg < L(0.0)) ? M::pow_mq(L(1.0) - L(15.0) * mozg) : L(1.0) + L(4.7) * mozg;
   fhg = (iter == 1) ? fhgnew : L(0.5) * (fhg + fhgnew);
   T cwpc = M::sqrt(cwp * vai * hcan * fhg);
-  T tmp1 = M::exp(-cwpc * z0hg / hcan);
-  T tmp2 = M::exp(-cwpc * (z0h + zpd) / hcan);
-  T tmprah2 = hcan * M::exp(cwpc) / cwpc * (tmp1 - tmp2);
+  T tmp1 = M::exp(dv(-cwpc * z0hg, hcan));
+  T tmp2 = M::exp(dv(-cwpc * (z0h + zpd), hcan));
+  T tmprah2 = dv(hcan * M::exp(cwpc), cwpc) * (tmp1 - tmp2);
   T kh = rmax(KARMAN * fv * (hcan - zpd), mpe);
-  rahg = tmprah2 / kh;
-  T tmprb = cwpc * L(50.0) / (L(1.0) - M::exp(-cwpc / L(2.0)));
+  rahg = dv(tmprah2, kh);
+  T tmprb = dv(cwpc * L(50.0), L(1.0) - M::exp(-cwpc / L(2.0)));
   rb = tmprb * sqrt_dleaf_uc;
 }
 
@@ -1238,7 +1238,7 @@ DEV void sflx_column(const DevParams& P, const KArgs<T>& A, Col<T>& c, const Sin
           chv = chv / ur;
           cmv = cmv / ur;
         }
-        rahc = rmax(L(1.0), L(1.0) / (chv * ur));
+        rahc = rmax(L(1.0), dv(L(1.0), chv * ur));
         T rawc = rahc;
         ragrb<T, R>(sqrt_dleaf_uc, iter, vaie, rhoair, hg, c.tah, zpd, z0mg, z0mg, hcan, z0h, fv,
                     cwp, mpe, fhg, rahg, rb);
@@ -1259,43 +1259,43 @@ DEV void sflx_column(const DevParams& P, const KArgs<T>& A, Col<T>& c, const Sin
             canres<T, R>(V, c.sfcprs, c.tv, parsha, c.eah, btran, rssha, psnsha);
           }
         }
-        cah = L(1.0) / rahc;
-        cvh = L(2.0) * vaie / rb;
-        T cgh = L(1.0) / rahg;
+        cah = dv(L(1.0), rahc);
+        cvh = dv(L(2.0) * vaie, rb);
+        T cgh = dv(L(1.0), rahg);
         T cond = cah + cvh + cgh;
-        T ata = (c.sfctmp * cah + tgv * cgh) / cond;
-        T bta = cvh / cond;
+        T ata = dv(c.sfctmp * cah + tgv * cgh, cond);
+        T bta = dv(cvh, cond);
         T csh = (L(1.0) - bta) * rhoair * CPAIR * cvh;
-        T caw = L(1.0) / rawc;
-        T cew = c.fwet * vaie / rb;
-        T ctw = (L(1.0) - c.fwet) * (laisune / (rb + rssun) + laishae / (rb + rssha));
-        T cgw = L(1.0) / (rawg + rsurf);
+        T caw = dv(L(1.0), rawc);
+        T cew = dv(c.fwet * vaie, rb);
+        T ctw = (L(1.0) - c.fwet) * (dv(laisune, rb + rssun) + dv(laishae, rb + rssha));
+        T cgw = dv(L(1.0), rawg + rsurf);
         cond = caw + cew + ctw + cgw;
-        T aea = (eair * caw + estg * cgw) / cond;
-        T bea = (cew + ctw) / cond;
-        T cev = (L(1.0) - bea) * cew * rhoair * CPAIR / gammav;
-        T ctr = (L(1.0) - bea) * ctw * rhoair * CPAIR / gammav;
+        T aea = dv(eair * caw + estg * cgw, cond);
+        T bea = dv(cew + ctw, cond);
+        T cev = dv((L(1.0) - bea) * cew * rhoair * CPAIR, gammav);
+        T ctr = dv((L(1.0) - bea) * ctw * rhoair * CPAIR, gammav);
         c.tah = ata + bta * c.tv;
         c.eah = aea + bea * estv;
         irc = fveg * (air + cir * p4(c.tv));
         shc = fveg * rhoair * CPAIR * cvh * (c.tv - c.tah);
-        evc = fveg * rhoair * CPAIR * cew * (estv - c.eah) / gammav;
-        tr = fveg * rhoair * CPAIR * ctw * (estv - c.eah) / gammav;
+        evc = dv(fveg * rhoair * CPAIR * cew * (estv - c.eah), gammav);
+        tr = dv(fveg * rhoair * CPAIR * ctw * (estv - c.eah), gammav);
         if (c.tv > TFRZ)
-          evc = rmin(c.canliq * latheav / DT, evc);
+          evc = rmin(dv(c.canliq * latheav, DT), evc);
         else
-          evc = rmin(c.canice * latheav / DT, evc);
+          evc = rmin(dv(c.canice * latheav, DT), evc);
         T b = sav - irc - shc - evc - tr;
         T a = fveg * (L(4.0) * cir * p3(c.tv) + csh + (cev + ctr) * destv);
-        T dtv = b / a;
+        T dtv = dv(b, a);
         irc = irc + fveg * L(4.0) * cir * p3(c.tv) * dtv;
         shc = shc + fveg * csh * dtv;
         evc = evc + fveg * cev * destv * dtv;
         tr = tr + fveg * ctr * destv * dtv;
         c.tv = c.tv + dtv;
-        h = rhoair * CPAIR * (c.tah - c.sfctmp) / rahc;
-        hg = rhoair * CPAIR * (tgv - c.tah) / rahg;
-        c.qsfc = (L(0.622) * c.eah) / (c.sfcprs - L(0.378) * c.eah);
+        h = dv(rhoair * CPAIR * (c.tah - c.sfctmp), rahc);
+        hg = dv(rhoair * CPAIR * (tgv - c.tah), rahg);
+        c.qsfc = dv(L(0.622) * c.eah, c.sfcprs - L(0.378) * c.eah);
         return dtv;
     };
     vtrips = 1;
@@ -1398,7 +1398,7 @@ DEV void sflx_column(const DevParams& P, const KArgs<T>& A, Col<T>& c, const Sin
       ghv = cgh * (tgv - stc_top);
       T b = sag - irg - shg - evg - ghv;
       T a = L(4.0) * cir * p3(tgv) + csh + cev * destg + cgh;
-      T dtg = b / a;
+      T dtg = dv(b, a);
       irg = irg + L(4.0) * cir * p3(tgv) * dtg;
       shg = shg + csh * dtg;
       evg = evg + cev * destg * dtg;
@@ -1461,20 +1461,20 @@ DEV void sflx_column(const DevParams& P, const KArgs<T>& A, Col<T>& c, const Sin
           chb = rmin(L(0.01), chb);
         }
       }
-      T rahb = rmax(L(1.0), L(1.0) / (chb * ur));
+      T rahb = rmax(L(1.0), dv(L(1.0), chb * ur));
       T rawb = rahb;
-      ehb = L(1.0) / rahb;
+      ehb = dv(L(1.0), rahb);
       estg = es_tgb;
       const T destg = des_tgb;
-      csh = rhoair * CPAIR / rahb;
-      cev = rhoair * CPAIR / gammag / (rsurf + rawb);
+      csh = dv(rhoair * CPAIR, rahb);
+      cev = dv(dv(rhoair * CPAIR, gammag), rsurf + rawb);
       irb = cir * p4(tgb) - emg * c.lwdn;
       shb = csh * (tgb - c.sfctmp);
       evb = cev * (estg * rhsur - eair);
       ghb = cgh * (tgb - stc_top);
       T b = sag - irb - shb - evb - ghb;
       T a = L(4.0) * cir * p3(tgb) + csh + cev * destg + cgh;
-      T dtg = b / a;
+      T dtg = dv(b, a);
       irb = irb + L(4.0) * cir * p3(tgb) * dtg;
       shb = shb + csh * dtg;
       evb = evb + cev * destg * dtg;

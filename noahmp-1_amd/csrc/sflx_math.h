@@ -113,6 +113,40 @@ __device__ __forceinline__ T p4(T x) { return x * p3(x); }
 template <class T>
 __device__ __forceinline__ T p5(T x) { return x * p4(x); }
 
+// Division in the Newton loops (vege_flux, bare_flux, sfcdif1, ragrb).  fp32
+// (the bit-exact path): IEEE `/`.  fp64 (held to tolerances, not bits): the
+// reciprocal from v_rcp_f64 refined by two Newton steps, times the numerator,
+// plus one residual correction -- within 1 ulp of the IEEE quotient, in 9
+// instructions instead of the div_scale/div_fmas/div_fixup sequence's 13, and
+// without its vcc chain.  v_div_fixup_f64 gives zero, infinite and NaN
+// operands (and overflow) their IEEE results and the quotient its sign.  (A
+// branch back to IEEE `/` for non-finite results instead measured slower than
+// plain `/`: profiles/r02/fp64_div.txt.)
+template <class T>
+__device__ __forceinline__ T dv(T a, T b) {
+  return a / b;
+}
+template <>
+__device__ __forceinline__ double dv<double>(double a, double b) {
+#ifdef NMP_F64_IEEE_DIV
+  return a / b;
+#else
+  double r = __builtin_amdgcn_rcp(b);
+  double e = __builtin_fma(-b, r, 1.0);
+  r = __builtin_fma(r, e, r);
+  e = __builtin_fma(-b, r, 1.0);
+  r = __builtin_fma(r, e, r);
+  double q = a * r;
+  e = __builtin_fma(-b, q, a);
+  q = __builtin_fma(e, r, q);
+#ifdef NMP_F64_DV_NOGUARD
+  return q;
+#else
+  return __builtin_amdgcn_div_fixup(q, b, a);
+#endif
+#endif
+}
+
 // Register-array access with a runtime index, lowered to a select chain so the
 // array itself stays in VGPRs (a dynamic subscript would demote it to scratch).
 // The empty asm pins each element as a register value: without it InstCombine

@@ -8,6 +8,7 @@
 //   tdfcnd func.f90:1500-1595   soil thermal conductivity
 //   frh2o  func.f90:4494-4598   supercooled soil water (Newton + Flerchinger)
 //   rosr12 func.f90:4240-4288   tridiagonal (Thomas) solve on layers kt..6
+//   dv     the fp64 Newton-loop division (csrc/sflx_math.h), against IEEE `/`
 // tests/test_gpu_routines.py compares them bit for bit with the oracle's C
 // restatement of each routine, and frh2o also with the reference's own
 // (public) frh2o.  Built by __graft_entry__.build() into tests/lib/.
@@ -76,6 +77,13 @@ __global__ void k_rosr12(int n, const int* kt, const float* a, const float* b, f
     delta[7 * i + k] = de[k];
     c[7 * i + k] = cc[k];  // intent(inout) in the reference
   }
+}
+
+__global__ void k_dv64(int n, const double* a, const double* b, double* q, double* ieee) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  q[i] = nmp::dv<double>(a[i], b[i]);
+  ieee[i] = a[i] / b[i];
 }
 
 // host helpers: device copies in, one launch, results out (synchronous)
@@ -159,6 +167,17 @@ int rt_rosr12(int n, const int* kt, const float* a, const float* b, float* c, co
   if (finish(D, p, dp, m) != 0) return -4;
   if (hipMemcpy(c, dc, m * sizeof(float), hipMemcpyDeviceToHost) != hipSuccess) return -4;
   return hipMemcpy(delta, de, m * sizeof(float), hipMemcpyDeviceToHost) == hipSuccess ? 0 : -4;
+}
+
+int rt_dv64(int n, const double* a, const double* b, double* q, double* ieee) {
+  Dev D;
+  const double *da = D.in(a, n), *db = D.in(b, n);
+  double *dq = D.in<double>(nullptr, n), *di = D.in<double>(nullptr, n);
+  if (!da || !db || !dq || !di) return -4;
+  hipLaunchKernelGGL(k_dv64, dim3((n + 255) / 256), dim3(256), 0, 0, n, da, db, dq, di);
+  if (hipDeviceSynchronize() != hipSuccess) return -4;
+  if (hipMemcpy(q, dq, n * sizeof(double), hipMemcpyDeviceToHost) != hipSuccess) return -4;
+  return hipMemcpy(ieee, di, n * sizeof(double), hipMemcpyDeviceToHost) == hipSuccess ? 0 : -4;
 }
 
 }  // extern "C"

@@ -86,6 +86,8 @@ def rt():
     lib.rt_tdfcnd.argtypes = [C.c_void_p, C.c_int, i32p, f32p, f32p, f32p]
     lib.rt_frh2o.argtypes = [C.c_void_p, C.c_int, i32p, f32p, f32p, f32p, f32p, i32p]
     lib.rt_rosr12.argtypes = [C.c_int, i32p, f32p, f32p, f32p, f32p, f32p, f32p]
+    f64p = np.ctypeslib.ndpointer(np.float64, flags="C_CONTIGUOUS")
+    lib.rt_dv64.argtypes = [C.c_int, f64p, f64p, f64p, f64p]
     return lib
 
 
@@ -143,3 +145,37 @@ def test_device_rosr12_vs_restatement(rt, oracle_port):
     assert bit_equal(p[act], wp[act]).all()
     assert bit_equal(dl[act], wd[act]).all()
     assert bit_equal(cg[:, 6], wc[:, 6]).all()  # C(NSOIL) = 0 on exit
+
+
+@pytest.mark.gpu
+def test_device_fp64_loop_division(rt):
+    """nmp::dv<double> (the fp64 path's Newton-loop division, csrc/sflx_math.h):
+    within 1 ulp of IEEE a/b on finite operands over 40 decades (0 ulp on
+    most), and exactly IEEE's value -- sign included -- for zero, infinite and
+    NaN operands and for overflow and underflow."""
+    rng = np.random.default_rng(9)
+    n = 200_000
+    a = rng.choice([-1.0, 1.0], n) * 10.0 ** rng.uniform(-20, 20, n)
+    b = rng.choice([-1.0, 1.0], n) * 10.0 ** rng.uniform(-20, 20, n)
+    inf, nan = np.inf, np.nan
+    sa = np.array([0.0, -0.0, 1.0, -1.0, inf, -inf, 1.0, 0.0, inf, nan, 1.0, 1e300, 1e-300, 3.0,
+                   -0.0, 5.0])
+    sb = np.array([2.0, 2.0, 0.0, 0.0, 2.0, 3.0, inf, 0.0, inf, 1.0, nan, 1e-300, 1e300, -inf,
+                   -4.0, -0.0])
+    a = np.ascontiguousarray(np.concatenate([a, sa]))
+    b = np.ascontiguousarray(np.concatenate([b, sb]))
+    q = np.zeros_like(a)
+    ieee = np.zeros_like(a)
+    assert rt.rt_dv64(a.size, a, b, q, ieee) == 0
+    with np.errstate(all="ignore"):
+        host = a / b
+    # the device's IEEE division is the host's
+    assert np.array_equal(ieee, host, equal_nan=True)
+    fin = np.isfinite(host) & (host != 0)
+    ulp = np.abs(q[fin] - host[fin]) / np.spacing(np.abs(host[fin]))
+    assert ulp.max() <= 1.0, ulp.max()
+    assert (ulp == 0).mean() > 0.9
+    sp = ~fin
+    assert np.array_equal(q[sp], host[sp], equal_nan=True)
+    num = sp & ~np.isnan(host)  # (a NaN's sign bit is not specified)
+    assert np.array_equal(np.signbit(q[num]), np.signbit(host[num]))

@@ -62,6 +62,8 @@ VARIANTS = {
     "vu2": ("-DNMP_VEGE_UNROLL=2",),
     "vu3": ("-DNMP_VEGE_UNROLL=3",),
     "pinnv": ("-DNMP_PIN_NONVOLATILE",),
+    "dvnoguard": ("-DNMP_F64_DV_NOGUARD",),
+    "dvieee": ("-DNMP_F64_IEEE_DIV",),
 }
 if __name__ == "__main__":
     names = sys.argv[1:] or list(VARIANTS)
