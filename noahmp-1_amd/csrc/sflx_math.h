@@ -37,7 +37,15 @@ struct Mth<double, REF> {
   NMP_MATH_FN double exp2(double x) { return ::exp2(x); }
   NMP_MATH_FN double log(double x) { return ::log(x); }
   NMP_MATH_FN double log10(double x) { return ::log10(x); }
+#ifdef NMP_F64_OCML_POW
   NMP_MATH_FN double pow(double x, double y) { return ::pow(x, y); }
+#else
+  // x**y as exp(y log x): within |y log x| ulp of pow, which is far inside the
+  // fp64 path's tolerances, at about half the cost of ocml's double pow (that
+  // one carries log x in double-double).  Every base in the kernel is >= 0;
+  // 0**y (y > 0) -> exp(-inf) = 0 as pow gives.
+  NMP_MATH_FN double pow(double x, double y) { return ::exp(y * ::log(x)); }
+#endif
   // x**0.25 and x**(-0.25): the fp64 path is held to a tolerance, not to bits
   // (DESIGN.md "fp64"), so the fourth root is two square roots (<= 1 ulp from
   // pow, and ~10x cheaper than ocml's double pow)

@@ -64,6 +64,7 @@ VARIANTS = {
     "pinnv": ("-DNMP_PIN_NONVOLATILE",),
     "dvnoguard": ("-DNMP_F64_DV_NOGUARD",),
     "dvieee": ("-DNMP_F64_IEEE_DIV",),
+    "ocmlpow": ("-DNMP_F64_OCML_POW",),
 }
 if __name__ == "__main__":
     names = sys.argv[1:] or list(VARIANTS)

@@ -32,12 +32,16 @@ def main():
     if order != "as-generated":  # the bench's default column order
         from noahmp_amd.order import coherent_order
         cols = cols.take(coherent_order(cols.lon, cols.static_i, cols.isnow, order))
-    eng = Engine(P, L.CASE_NML_OPTIONS, 0, 4, math)
+    precision = int(sys.argv[5]) if len(sys.argv) > 5 else 4
+    opt_veg = int(sys.argv[6]) if len(sys.argv) > 6 else 1
+    dtype = torch.float32 if precision == 4 else torch.float64
+    eng = Engine(P, dict(L.CASE_NML_OPTIONS, opt_veg=opt_veg), 0, precision,
+                 math if precision == 4 else "ref")
     lib = eng._lib
     lib.nmp_debug_phase_cycles.argtypes = [C.c_void_p, C.c_int]
-    cs = ColumnState.from_host(cols, "cuda:0")
+    cs = ColumnState.from_host(cols, "cuda:0", dtype)
     F = [torch.as_tensor(cases.forcing_step(cols, 180.0 + s / 48.0, 366, s, seed=1000),
-                         device="cuda:0") for s in range(8)]
+                         device="cuda:0").to(dtype) for s in range(8)]
     buf = (C.c_ulonglong * 16)()
     for s in range(10):
         if s == 2:
@@ -48,7 +52,8 @@ def main():
     lib.nmp_debug_phase_cycles(buf, 0)
     v = np.array(list(buf), dtype=np.float64)
     tot = v.sum()
-    print(f"ncol={n} kind={kind} math={math} order={order}: wave-cycles per column-step "
+    print(f"ncol={n} kind={kind} math={math} order={order} precision={precision} "
+          f"opt_veg={opt_veg}: wave-cycles per column-step "
           f"{tot / (8 * n / 64) / 64:.0f} (per lane-equivalent)")
     for i in np.argsort(-v):
         if v[i] > 0:
