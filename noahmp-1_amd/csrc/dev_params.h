@@ -9,6 +9,8 @@
 #pragma once
 #include <stdint.h>
 
+#include <cmath>
+
 #include "glibc_math.h"
 #include "noahmp_engine.h"
 
@@ -35,6 +37,8 @@ struct SoilRec {  // one soil type (soil_param.f90:13-23)
   // the host with the glibc-exact libm: THKS**(1-SMCMAX) and THKDRY
   float tdf_thks_pow, tdf_thkdry;
   float rsurf_den;  // 2.2E-5*SMCMAX**2*(1-SMCWLT/SMCMAX)**(2+3/BEXP) (rsurf :1150-1151)
+  // the same two tdfcnd factors in double for the fp64 path (host libm)
+  double tdf_thks_pow_d, tdf_thkdry_d;
 };
 
 struct GenRec {  // GENPARMMP.TBL scalars + soil colours (gen_param.f90:12-48, soil_param.f90:27-28)
@@ -88,6 +92,13 @@ inline void pack_dev_params(const nmp_params& p, DevParams& d) {
     r.tdf_thks_pow = gm::powf(thks, 1.0f - r.smcmax, T);
     const float gammd = (1.0f - r.smcmax) * 2700.0f;
     r.tdf_thkdry = (0.135f * gammd + 64.7f) / (2700.0f - 0.947f * gammd);
+    {
+      const double qz = r.quartz, smx = r.smcmax;
+      const double thks_d = std::pow(7.7, qz) * std::exp2(1.0 - qz);
+      r.tdf_thks_pow_d = std::pow(thks_d, 1.0 - smx);
+      const double gammd_d = (1.0 - smx) * 2700.0;
+      r.tdf_thkdry_d = (0.135 * gammd_d + 64.7) / (2700.0 - 0.947 * gammd_d);
+    }
     r.rsurf_den = 2.2E-5f * r.smcmax * r.smcmax *
                   gm::powf(1.0f - r.smcwlt / r.smcmax, 2.0f + 3.0f / r.bexp, T);
   }

@@ -104,6 +104,12 @@ DEV T tdfcnd(const SoilRec& S, T smc, T sh2o) {
     // soil-type-only factors precomputed on the host (dev_params.h), bit-identical
     thksat = (T)S.tdf_thks_pow * M::pow(TKICE, smcmax - xu) * M::pow(thkw, xu);
     thkdry = (T)S.tdf_thkdry;
+  } else if constexpr (sizeof(T) == 8) {
+    // fp64 (tolerance path): the type-only factors from the host in double, and
+    // TKICE**(SMCMAX-XU) * THKW**XU as one exp with the logs of the constants
+    thksat = (T)S.tdf_thks_pow_d *
+             M::exp((smcmax - xu) * 0.7884573603642703 + xu * -0.5621189181535413);
+    thkdry = (T)S.tdf_thkdry_d;
   } else {
     T thks = M::pow(thkqtz, quartz) * M::exp2(L(1.0) - quartz);  // 2.0**x -> exp2
     thksat = M::pow(thks, L(1.0) - smcmax) * M::pow(TKICE, smcmax - xu) * M::pow(thkw, xu);
