@@ -17,8 +17,16 @@ LIB_DIR = os.path.join(PKG, "lib")
 DEFAULT_LIB_PATH = os.path.join(LIB_DIR, "libnoahmp_engine.so")
 # NOAHMP_ENGINE_LIB: a tuning variant (tools/build_variants.py), hash-checked only on request
 LIB_PATH = os.environ.get("NOAHMP_ENGINE_LIB") or DEFAULT_LIB_PATH
-SOURCES = ["engine.hip", "sflx_kernel.hip", "rebin.hip", "forcing.hip", "tables.cpp"]
+SOURCES = ["engine.hip", "sflx_kernel.hip", "sflx_kernel_f64.hip", "rebin.hip", "forcing.hip",
+           "tables.cpp"]
 HEADERS = ["dev_params.h", "sflx_kargs.h", "sflx_math.h", "sflx_routines.h", "glibc_math.h"]
+# per-source flags: sflx_kernel.hip is compiled as the fp32 translation unit,
+# sflx_kernel_f64.hip (the same file, NMP_TU 8) as the fp64 one, in parallel.
+# The fp64 unit can take its own flags (tools/build_variants.py f64*): with
+# -freciprocal-math or -fapprox-func its divisions outside the Newton loops
+# become reciprocal sequences, which measured no faster on configs #2/#5
+# (profiles/r02/f64_flags_ab.txt), so it builds with the common flags.
+SOURCE_FLAGS = {"sflx_kernel.hip": ["-DNMP_TU=4"], "sflx_kernel_f64.hip": []}
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")
 FLAGS = ["-O3", f"--offload-arch={ARCH}", "-fPIC", "-shared", "-std=c++17",
@@ -29,12 +37,13 @@ FLAGS = ["-O3", f"--offload-arch={ARCH}", "-fPIC", "-shared", "-std=c++17",
          "-mllvm", "-disable-machine-licm"]
 
 
-def source_hash(extra: tuple = ()) -> str:
+def source_hash(extra: tuple = (), source_flags: dict | None = None) -> str:
     """Hash of every engine source + build flag: identifies the kernel a
     measurement (profiles/traffic.json) was taken on.  Compiled into the
     library (nmp_build_hash), so a stale library is detected at load time."""
     import hashlib
     h = hashlib.sha256(" ".join(FLAGS + list(extra)).encode())
+    h.update(repr(sorted((source_flags or SOURCE_FLAGS).items())).encode())
     for p in sorted(SOURCES + HEADERS):
         with open(os.path.join(CSRC, p), "rb") as f:
             h.update(f.read())
@@ -55,20 +64,41 @@ def built_hash(path: str = LIB_PATH) -> str | None:
 
 
 def build(force: bool = False, verbose: bool = True, out: str | None = None,
-          extra: tuple = ()) -> str:
-    """Build the engine library (default: LIB_PATH; `out`/`extra` for tuning variants)."""
+          extra: tuple = (), source_flags: dict | None = None) -> str:
+    """Build the engine library (default: LIB_PATH; `out`/`extra`/`source_flags`
+    for tuning variants)."""
     path = out or LIB_PATH
-    want = source_hash(extra)
+    sflags = source_flags or SOURCE_FLAGS
+    want = source_hash(extra, sflags)
     if not force and built_hash(path) == want:
         return path
     os.makedirs(os.path.dirname(path), exist_ok=True)
     tmp = path + ".tmp"
-    cmd = [HIPCC, *FLAGS, *extra, f'-DNMP_BUILD_HASH="{want}"', "-I", os.path.join(ROOT, "include"), "-I", CSRC, "-o", tmp,
-           *[os.path.join(CSRC, s) for s in SOURCES]]
+    objdir = tmp + ".objs"
+    os.makedirs(objdir, exist_ok=True)
+    inc = ["-I", os.path.join(ROOT, "include"), "-I", CSRC]
+    cmds = []
+    for src in SOURCES:
+        obj = os.path.join(objdir, src + ".o")
+        cflags = [f for f in FLAGS if f != "-shared"]
+        cmds.append((obj, [HIPCC, *cflags, *sflags.get(src, []), *extra,
+                           f'-DNMP_BUILD_HASH="{want}"', *inc, "-c", "-o", obj,
+                           os.path.join(CSRC, src)]))
     if verbose:
-        print("[noahmp build]", " ".join(cmd), flush=True)
-    subprocess.run(cmd, check=True)
+        for _, c in cmds:
+            print("[noahmp build]", " ".join(c), flush=True)
+    from concurrent.futures import ThreadPoolExecutor
+    jobs = int(os.environ.get("MAX_JOBS", "0")) or min(len(cmds), os.cpu_count() or 1)
+    with ThreadPoolExecutor(jobs) as ex:
+        for f in [ex.submit(subprocess.run, c, check=True) for _, c in cmds]:
+            f.result()
+    link = [HIPCC, *FLAGS, *extra, "-o", tmp, *[o for o, _ in cmds]]
+    if verbose:
+        print("[noahmp build]", " ".join(link), flush=True)
+    subprocess.run(link, check=True)
     os.replace(tmp, path)
+    import shutil
+    shutil.rmtree(objdir, ignore_errors=True)
     return path
 
 

@@ -808,11 +808,56 @@ struct Sink {
   }
 };
 
+// Layer-state copy in LDS (fp32 kernels): the 28 layer-state fields (STC,
+// ZSNSO, SNICE, SNLIQ, SH2O, SMC = state fields 0..27) are copied HBM -> LDS
+// at kernel entry by the load-to-LDS path (global_load_lds_dword, no VGPRs),
+// read from there into registers for the energy phase, and read from there
+// AGAIN after the flux loops instead of a second HBM read (the registers are
+// not held through the loops, DESIGN.md "Layer state across the flux loops").
+// Layout [field][thread] (28 x NMP_BLOCK floats, 28 KB per 256-thread block:
+// with the 11.5 KB of tables four blocks still fit a CU's 160 KB).  Each lane
+// reads back only its own slots, which its own copy wrote, so no barrier is
+// needed; nothing writes these fields before the second read.  (Issuing the
+// copy later, as a prefetch before the flux loops, does not hide its latency:
+// vmcnt counts in order, so the first spill reload after it waits for it.)
+#ifndef NMP_PREFETCH
+#define NMP_PREFETCH 3
+#endif
+constexpr int kPrefetchFields = NMP_S_SMC + 4;
+static_assert(NMP_S_STC == 0 && NMP_S_ZSNSO == 7 && NMP_S_SNICE == 14 && NMP_S_SNLIQ == 17 &&
+                  NMP_S_SH2O == 20 && NMP_S_SMC == 24,
+              "prefetch slots are state fields 0..27");
+template <class T, bool R>
+constexpr bool kPrefetch = NMP_PREFETCH != 0 && sizeof(T) == 4 && R;
+// (tuning: bit 0 = entry reads from the copy, bit 1 = the re-read from it)
+template <class T, bool R>
+constexpr bool kPfEntry = kPrefetch<T, R> && (NMP_PREFETCH & 1);
+template <class T, bool R>
+constexpr bool kPfReread = kPrefetch<T, R> && (NMP_PREFETCH & 2);
+typedef __attribute__((address_space(3))) float lds_f32;
+DEV lds_f32* lds_pool() {
+  __shared__ float pool[kPrefetchFields * NMP_BLOCK];
+  return (lds_f32*)pool;
+}
+template <class T>
+DEV void copy_layers_to_lds(const T* st, int64_t ld) {
+  lds_f32* pool = lds_pool();
+  const int wbase = __builtin_amdgcn_readfirstlane(threadIdx.x & ~63);
+  // laundered base: the 28 field addresses are not shared with (and kept live
+  // for) the step's other accesses to the same fields
+  __asm__ volatile("" : "+v"(st));
+#pragma unroll
+  for (int f = 0; f < kPrefetchFields; ++f)
+    __builtin_amdgcn_global_load_lds((const void*)(st + f * ld),
+                                     (__attribute__((address_space(3))) void*)(pool + f * NMP_BLOCK + wbase),
+                                     4, 0, 0);
+}
+
 // Optional per-phase timing (build with -DNMP_PHASE_TIMING; tools only):
 // each wave stamps s_memtime at phase boundaries and lane 0 accumulates the
 // deltas into nmp_phase_cycles[phase].  Compiled out otherwise.
 #ifdef NMP_PHASE_TIMING
-__device__ unsigned long long nmp_phase_cycles[16];
+static __device__ unsigned long long nmp_phase_cycles[16];
 struct PhaseClock {
   unsigned long long t;
   int ph;
@@ -1591,21 +1636,32 @@ DEV void sflx_column(const DevParams& P, const KArgs<T>& A, Col<T>& c, const Sin
   // Re-read the layer state (unchanged in HBM so far) instead of holding it in
   // registers through the flux iterations; then FICEOLD and thermoprop.
   {
+    // from the LDS copy (kPrefetch) or from HBM
     const T* st = out.fresh_state();
+    // the LDS slot index is laundered like fresh_state(): a real second read,
+    // not the entry values kept live in registers through the flux loops
+    int slot = threadIdx.x;
+    if constexpr (kPfReread<T, R>) __asm__ volatile("" : "+v"(slot));
+    auto rd = [&](int f) -> T {
+      if constexpr (kPfReread<T, R>)
+        return lds_pool()[f * NMP_BLOCK + slot];
+      else
+        return st[f * out.ld];
+    };
 #pragma unroll
     for (int k = 0; k < 7; ++k) {
-      c.stc[k] = st[(NMP_S_STC + k) * out.ld];
-      c.zsnso[k] = st[(NMP_S_ZSNSO + k) * out.ld];
+      c.stc[k] = rd(NMP_S_STC + k);
+      c.zsnso[k] = rd(NMP_S_ZSNSO + k);
     }
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
-      c.snice[k] = st[(NMP_S_SNICE + k) * out.ld];
-      c.snliq[k] = st[(NMP_S_SNLIQ + k) * out.ld];
+      c.snice[k] = rd(NMP_S_SNICE + k);
+      c.snliq[k] = rd(NMP_S_SNLIQ + k);
     }
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-      c.sh2o[k] = st[(NMP_S_SH2O + k) * out.ld];
-      c.smc[k] = st[(NMP_S_SMC + k) * out.ld];
+      c.sh2o[k] = rd(NMP_S_SH2O + k);
+      c.smc[k] = rd(NMP_S_SMC + k);
     }
     layer_dz(c);
   }
@@ -1620,7 +1676,7 @@ DEV void sflx_column(const DevParams& P, const KArgs<T>& A, Col<T>& c, const Sin
     for (int j = 0; j < 3; ++j)
       c.ficeold[j] = (j >= c.isnow + 3) ? c.snice[j] / (c.snice[j] + c.snliq[j]) : L(0.0);
   }
-  NMP_PHASE(1);
+  NMP_PHASE(14);
   // thermoprop + csnow + tdfcnd: func.f90:1341-1595
 #pragma unroll
   for (int j = 0; j < 3; ++j) {
@@ -2753,20 +2809,30 @@ void sflx_step_kernel(const DevParams* __restrict__ gparams,
   const int64_t ld = a.ld;
   Col<T> c;
   const T* st = a.state + c0;
+  {
+    // layer state: through the LDS copy (kPrefetch) or straight from HBM
+    if constexpr (kPrefetch<T, R>) copy_layers_to_lds(st, ld);
+    auto rd = [&](int f) -> T {
+      if constexpr (kPfEntry<T, R>)
+        return lds_pool()[f * NMP_BLOCK + threadIdx.x];
+      else
+        return st[f * ld];
+    };
 #pragma unroll
-  for (int k = 0; k < 7; ++k) {
-    c.stc[k] = st[(NMP_S_STC + k) * ld];
-    c.zsnso[k] = st[(NMP_S_ZSNSO + k) * ld];
-  }
+    for (int k = 0; k < 7; ++k) {
+      c.stc[k] = rd(NMP_S_STC + k);
+      c.zsnso[k] = rd(NMP_S_ZSNSO + k);
+    }
 #pragma unroll
-  for (int k = 0; k < 3; ++k) {
-    c.snice[k] = st[(NMP_S_SNICE + k) * ld];
-    c.snliq[k] = st[(NMP_S_SNLIQ + k) * ld];
-  }
+    for (int k = 0; k < 3; ++k) {
+      c.snice[k] = rd(NMP_S_SNICE + k);
+      c.snliq[k] = rd(NMP_S_SNLIQ + k);
+    }
 #pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    c.sh2o[k] = st[(NMP_S_SH2O + k) * ld];
-    c.smc[k] = st[(NMP_S_SMC + k) * ld];
+    for (int k = 0; k < 4; ++k) {
+      c.sh2o[k] = rd(NMP_S_SH2O + k);
+      c.smc[k] = rd(NMP_S_SMC + k);
+    }
   }
   c.tv = st[NMP_S_TV * ld]; c.tg = st[NMP_S_TG * ld];
   c.fwet = st[NMP_S_FWET * ld]; c.snowh = st[NMP_S_SNOWH * ld];
@@ -2833,22 +2899,51 @@ hipError_t launch_sflx(const DevParams* dparams, const KArgs<T>& a, hipStream_t 
 }
 
 #ifdef NMP_PHASE_TIMING
-extern "C" int nmp_debug_phase_cycles(unsigned long long* out16, int reset) {
-  if (hipMemcpyFromSymbol(out16, HIP_SYMBOL(nmp_phase_cycles), sizeof(unsigned long long) * 16) !=
-      hipSuccess)
-    return -4;
+// this translation unit's phase counters (added to out16; reset if asked)
+#define NMP_PC_CAT2(a, b) a##b
+#define NMP_PC_CAT(a, b) NMP_PC_CAT2(a, b)
+#ifdef NMP_TU
+#define NMP_TU_ID NMP_TU
+#else
+#define NMP_TU_ID 0
+#endif
+int NMP_PC_CAT(phase_cycles_tu, NMP_TU_ID)(unsigned long long* out16, int reset) {
+  unsigned long long v[16];
+  if (hipMemcpyFromSymbol(v, HIP_SYMBOL(nmp_phase_cycles), sizeof(v)) != hipSuccess) return -4;
+  for (int i = 0; i < 16; ++i) out16[i] += v[i];
   if (reset) {
     unsigned long long z[16] = {0};
     if (hipMemcpyToSymbol(HIP_SYMBOL(nmp_phase_cycles), z, sizeof(z)) != hipSuccess) return -4;
   }
   return 0;
 }
+#if !defined(NMP_TU)
+extern "C" int nmp_debug_phase_cycles(unsigned long long* out16, int reset) {
+  for (int i = 0; i < 16; ++i) out16[i] = 0;
+  return phase_cycles_tu0(out16, reset);
+}
+#elif NMP_TU == 4
+int phase_cycles_tu8(unsigned long long* out16, int reset);
+extern "C" int nmp_debug_phase_cycles(unsigned long long* out16, int reset) {
+  for (int i = 0; i < 16; ++i) out16[i] = 0;
+  const int r = phase_cycles_tu4(out16, reset);
+  return r ? r : phase_cycles_tu8(out16, reset);
+}
 #endif
+#endif
+
+// Instantiations.  The library compiles this file twice (build.py): NMP_TU 4
+// for the fp32 kernels and NMP_TU 8 (sflx_kernel_f64.hip) for the fp64 ones,
+// each with its own flags; without NMP_TU one object holds both.
+#if !defined(NMP_TU) || NMP_TU == 4
 template hipError_t launch_sflx<float, true>(const DevParams*, const KArgs<float>&, hipStream_t,
                                              bool, int);
 template hipError_t launch_sflx<float, false>(const DevParams*, const KArgs<float>&, hipStream_t,
                                               bool, int);
+#endif
+#if !defined(NMP_TU) || NMP_TU == 8
 template hipError_t launch_sflx<double, false>(const DevParams*, const KArgs<double>&, hipStream_t,
                                                bool, int);
+#endif
 
 }  // namespace nmp

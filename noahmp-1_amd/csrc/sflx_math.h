@@ -78,8 +78,8 @@ struct Mth<float, false> {
 
 // glibc libm tables: one __constant__ master copy, staged into LDS by every
 // workgroup's prologue (stage_math_tables) before first use.
-__shared__ gm::GmTables gm_lds;
-__constant__ gm::GmTables gm_const = {GM_EXP2F_TAB, GM_LOGF_TAB, GM_POWF_TAB};
+static __shared__ gm::GmTables gm_lds;
+static __constant__ gm::GmTables gm_const = {GM_EXP2F_TAB, GM_LOGF_TAB, GM_POWF_TAB};
 
 __device__ __forceinline__ void stage_math_tables() {
   constexpr int NW = sizeof(gm::GmTables) / sizeof(int4);

@@ -17,6 +17,13 @@ VARIANTS = {
     "w1": ("-DNMP_WAVES_PER_EU=1",),
     "w3": ("-DNMP_WAVES_PER_EU=3",),
     "phase": ("-DNMP_PHASE_TIMING",),
+    "phase_nopf": ("-DNMP_PHASE_TIMING", "-DNMP_PREFETCH=0"),
+    "nopf": ("-DNMP_PREFETCH=0",),
+    "pf1": ("-DNMP_PREFETCH=1",),
+    # fp64 translation unit flags (the fp32 kernels unchanged)
+    "f64ieee": {"f64": []},
+    "f64afn": {"f64": ["-freciprocal-math", "-fapprox-func"]},
+    "pf2": ("-DNMP_PREFETCH=2",),
     "b128": ("-DNMP_BLOCK=128",),
     "b64": ("-DNMP_BLOCK=64",),
     "b512": ("-DNMP_BLOCK=512",),
@@ -69,8 +76,15 @@ VARIANTS = {
 if __name__ == "__main__":
     names = sys.argv[1:] or list(VARIANTS)
     vdir = os.path.join(build.LIB_DIR, "variants")
-    with ThreadPoolExecutor(4) as ex:
-        list(ex.map(lambda n: build.build(force=True, verbose=False,
-                                          out=os.path.join(vdir, f"lib_{n}.so"),
-                                          extra=VARIANTS[n]), names))
+    def one(n):
+        v = VARIANTS[n]
+        if isinstance(v, dict):  # per-source flags: {"extra": (...), "f64": [...]}
+            sf = dict(build.SOURCE_FLAGS)
+            if "f64" in v:
+                sf["sflx_kernel_f64.hip"] = list(v["f64"])
+            return build.build(force=True, verbose=False, out=os.path.join(vdir, f"lib_{n}.so"),
+                               extra=tuple(v.get("extra", ())), source_flags=sf)
+        return build.build(force=True, verbose=False, out=os.path.join(vdir, f"lib_{n}.so"), extra=v)
+    with ThreadPoolExecutor(2) as ex:
+        list(ex.map(one, names))
     print("built", names)

@@ -17,9 +17,9 @@ from noahmp_amd import cases, layout as L  # noqa: E402
 from noahmp_amd.engine import ColumnState, Engine  # noqa: E402
 from noahmp_amd.params import Params  # noqa: E402
 
-NAMES = ["prelude(atm,phenology,fveg,fsno)", "thermoprop", "radiation", "btran+rsurf",
+NAMES = ["prelude(atm,phenology,fveg,fsno)", "df_top (first-layer conductivity)", "radiation", "btran+rsurf",
          "vege_flux", "bare_flux", "aggregate", "tsnosoi", "phasechange", "canwater",
-         "snowwater", "frozen ground", "soilh2o+groundwater", "carbon+checks", "-", "-"]
+         "snowwater", "frozen ground", "soilh2o+groundwater", "carbon+checks", "thermoprop", "-"]
 
 
 def main():
