@@ -19,6 +19,7 @@ VARIANTS = {
     "phase": ("-DNMP_PHASE_TIMING",),
     "phase_nopf": ("-DNMP_PHASE_TIMING", "-DNMP_PREFETCH=0"),
     "nopf": ("-DNMP_PREFETCH=0",),
+    "nt0": ("-DNMP_NT=0",),
     "pf1": ("-DNMP_PREFETCH=1",),
     # fp64 translation unit flags (the fp32 kernels unchanged)
     "f64ieee": {"f64": []},
