@@ -896,6 +896,16 @@ struct PhaseClock {
 #ifndef NMP_VEGE_UNROLL
 #define NMP_VEGE_UNROLL 1
 #endif
+// Unroll factors of the fixed 5-iteration under-canopy (loop2) and bare_flux
+// Newton loops (tuning knobs, results identical).  bare_flux is unrolled in
+// the fp32 kernels: config #3 +0.8 %, fewer spills (59 -> 52); fp64 and
+// loop2 measured no gain (profiles/r02/unroll_ab.txt).
+#ifndef NMP_LOOP2_UNROLL
+#define NMP_LOOP2_UNROLL 1
+#endif
+#ifndef NMP_BARE_UNROLL
+#define NMP_BARE_UNROLL sizeof(T) == 4 ? 5 : 1
+#endif
 #define NMP_STR(x) #x
 #define NMP_UNROLL(n) _Pragma(NMP_STR(unroll n))
 
@@ -1451,7 +1461,7 @@ DEV void sflx_column(const DevParams& P, const KArgs<T>& A, Col<T>& c, const Sin
     T csh = rhoair * CPAIR / rahg;
     T cev = rhoair * CPAIR / (gammag * (rahg + rsurf));
     T cgh = L(2.0) * df_top / dz_top;
-#pragma unroll 1
+NMP_UNROLL(NMP_LOOP2_UNROLL)
     for (int iter = 1; iter <= 5; ++iter) {
       tt = tdc(tgv);
       T destg;
@@ -1494,6 +1504,7 @@ DEV void sflx_column(const DevParams& P, const KArgs<T>& A, Col<T>& c, const Sin
 
   NMP_PHASE(5);
   // ---- bare_flux: func.f90:2967-3257 ----
+  constexpr int kBareUnroll = NMP_BARE_UNROLL;
   T tgb = c.tg, cmb = c.cm, chb = c.ch;
   T irb, shb, evb, ghb, t2mb = L(0.0), q2b = L(0.0), chb2 = L(0.0);
   {
@@ -1511,7 +1522,7 @@ DEV void sflx_column(const DevParams& P, const KArgs<T>& A, Col<T>& c, const Sin
     irb = shb = evb = ghb = L(0.0);
     const Sfc1Logs<T, R> lgb = (o.sfc == 1) ? Sfc1Logs<T, R>(zlvl, zpdg, z0mg, z0h, c.status)
                                             : Sfc1Logs<T, R>{};
-#pragma unroll 1
+NMP_UNROLL(kBareUnroll)
     for (int iter = 1; iter <= 5; ++iter) {
       if (o.sfc == 1)
         sfcdif1<T, R>(iter, c.sfctmp, rhoair, h, qair, zlvl, zpdg, lgb, z0h, ur, mpe, moz,

@@ -20,6 +20,9 @@ VARIANTS = {
     "phase_nopf": ("-DNMP_PHASE_TIMING", "-DNMP_PREFETCH=0"),
     "nopf": ("-DNMP_PREFETCH=0",),
     "nt0": ("-DNMP_NT=0",),
+    "u_l2": ("-DNMP_LOOP2_UNROLL=5",),
+    "u_bare": ("-DNMP_BARE_UNROLL=5",),
+    "u_both": ("-DNMP_LOOP2_UNROLL=5", "-DNMP_BARE_UNROLL=5"),
     "pf1": ("-DNMP_PREFETCH=1",),
     # fp64 translation unit flags (the fp32 kernels unchanged)
     "f64ieee": {"f64": []},
