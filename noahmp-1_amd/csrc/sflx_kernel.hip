@@ -892,6 +892,17 @@ struct PhaseClock {
 #define NMP_PHASE(i) ((void)0)
 #endif
 
+// Optional per-wave timing (build with -DNMP_WAVE_TIMING; tools only): each
+// wave records {start, end} of s_memrealtime (100 MHz, one clock for the whole
+// chip), its HW_ID/XCC_ID and {block, launch tag} into nmp_wave_rec, so that
+// tools/wave_timeline.py can measure how full the wave slots stay over a launch
+// (tail and workgroup-granularity idle time).  Compiled out otherwise.
+#ifdef NMP_WAVE_TIMING
+#define NMP_WAVE_REC_MAX (1 << 17)
+static __device__ unsigned long long nmp_wave_rec[4 * NMP_WAVE_REC_MAX];
+static __device__ unsigned int nmp_wave_ctr;
+#endif
+
 // Unroll factor of the vege_flux Newton loop (tuning knob, results identical).
 #ifndef NMP_VEGE_UNROLL
 #define NMP_VEGE_UNROLL 1
@@ -2809,6 +2820,9 @@ __global__ __launch_bounds__(NMP_BLOCK)
 __attribute__((amdgpu_waves_per_eu(waves_per_eu<T>(SMALL))))
 void sflx_step_kernel(const DevParams* __restrict__ gparams,
                                                           KArgs<T> a) {
+#ifdef NMP_WAVE_TIMING
+  const unsigned long long wt0 = __builtin_amdgcn_s_memrealtime();
+#endif
   __shared__ __attribute__((aligned(16))) DevParams sp;
   {
     const int4* src = reinterpret_cast<const int4*>(gparams);
@@ -2892,6 +2906,24 @@ void sflx_step_kernel(const DevParams* __restrict__ gparams,
   sflx_column<T, R, OS>(sp, a, c, out);
 
   if (c.status != 0) a.status[c0] |= c.status;
+#ifdef NMP_WAVE_TIMING
+  {
+    const unsigned long long wt1 = __builtin_amdgcn_s_memrealtime();
+    if (lane == 0) {
+      const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_REG_HW_ID
+      const unsigned xcc = __builtin_amdgcn_s_getreg((3 << 11) | 20);  // HW_REG_XCC_ID
+      const unsigned i = atomicAdd(&nmp_wave_ctr, 1u);
+      if (i < NMP_WAVE_REC_MAX) {
+        unsigned long long* r = nmp_wave_rec + 4 * (size_t)i;
+        r[0] = wt0;
+        r[1] = wt1;
+        r[2] = (unsigned long long)hw | ((unsigned long long)xcc << 32);
+        r[3] = (unsigned long long)blockIdx.x |
+               ((unsigned long long)(((uintptr_t)a.state >> 8) & 0xffffffffu) << 32);
+      }
+    }
+  }
+#endif
 }
 
 // launch wrapper (one instantiation per precision / math policy)
@@ -2960,6 +2992,27 @@ extern "C" int nmp_debug_phase_cycles(unsigned long long* out16, int reset) {
   return r ? r : phase_cycles_tu8(out16, reset);
 }
 #endif
+#endif
+
+#if defined(NMP_WAVE_TIMING) && (!defined(NMP_TU) || NMP_TU == 4)
+// the fp32 kernels' wave records: copies min(count, max_rec) records of 4 u64
+// into out and returns the number recorded since the last reset (may exceed
+// the buffer's NMP_WAVE_REC_MAX); reset clears the counter afterwards
+extern "C" long long nmp_debug_wave_records(unsigned long long* out, long long max_rec, int reset) {
+  unsigned int n = 0;
+  if (hipMemcpyFromSymbol(&n, HIP_SYMBOL(nmp_wave_ctr), sizeof(n)) != hipSuccess) return -4;
+  long long k = n < NMP_WAVE_REC_MAX ? n : NMP_WAVE_REC_MAX;
+  if (k > max_rec) k = max_rec;
+  if (out && k > 0 &&
+      hipMemcpyFromSymbol(out, HIP_SYMBOL(nmp_wave_rec), (size_t)k * 4 * sizeof(unsigned long long)) !=
+          hipSuccess)
+    return -4;
+  if (reset) {
+    const unsigned int z = 0;
+    if (hipMemcpyToSymbol(HIP_SYMBOL(nmp_wave_ctr), &z, sizeof(z)) != hipSuccess) return -4;
+  }
+  return n;
+}
 #endif
 
 // Instantiations.  The library compiles this file twice (build.py): NMP_TU 4

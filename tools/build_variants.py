@@ -76,6 +76,12 @@ VARIANTS = {
     "dvnoguard": ("-DNMP_F64_DV_NOGUARD",),
     "dvieee": ("-DNMP_F64_IEEE_DIV",),
     "ocmlpow": ("-DNMP_F64_OCML_POW",),
+    # per-wave start/end records (tools/wave_timeline.py)
+    "wt": ("-DNMP_WAVE_TIMING",),
+    "wt_b128": ("-DNMP_WAVE_TIMING", "-DNMP_BLOCK=128", "-DNMP_PREFETCH=0"),
+    "wt_b64": ("-DNMP_WAVE_TIMING", "-DNMP_BLOCK=64", "-DNMP_PREFETCH=0"),
+    "b128_nopf": ("-DNMP_BLOCK=128", "-DNMP_PREFETCH=0"),
+    "b64_nopf": ("-DNMP_BLOCK=64", "-DNMP_PREFETCH=0"),
 }
 if __name__ == "__main__":
     names = sys.argv[1:] or list(VARIANTS)
