@@ -158,6 +158,12 @@ def main():
     import torch.distributed as dist
     from noahmp_amd.engine import ColumnState, Engine, StreamShards
 
+    # NMP_BENCH_BACKEND=gloo: rehearsal of the N>1 control flow on fewer GPUs
+    # than ranks (ranks share devices, the gather is staged through the host);
+    # never a measurement -- RCCL refuses two ranks on one device
+    backend = os.environ.get("NMP_BENCH_BACKEND", "nccl")
+    if backend != "nccl":
+        local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     dtype = torch.float32 if a.precision == 4 else torch.float64
@@ -184,7 +190,10 @@ def main():
         # after the range streams exist: RCCL's communicator creates streams of
         # its own, and created first they left the two ranges sharing one of
         # the process's hardware queues (GPU_MAX_HW_QUEUES=4), serialising them
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
         # double-buffered output-step gather; a receiving rank's engine writes
         # straight into its own slot of the gather buffer (no local copy)
         gat = shard.DiagGather(L.NDIAG_OUT, world * n, dtype, dev, dst=gather_dst, comm=comm)
@@ -286,7 +295,8 @@ def main():
                        "rebin": {"tile": a.rebin_tile, "every": a.rebin_every}
                        if a.rebin_tile else None,
                        "parallelism": f"column-shard x{world}",
-                       "gather": a.gather if use_dist else None},
+                       "gather": a.gather if use_dist else None,
+                       "backend": backend if use_dist else None},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": "sflx_step_kernel", "kernel_ms": kern_ms,
