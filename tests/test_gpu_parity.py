@@ -638,6 +638,7 @@ def test_sflx_columns_caller_ficeold_vs_reference(engines):
     ("global", 1_036_800, 2, 4),       # config #5 grid + carbon, fp32
     ("global", 1_036_800, 2, 8),       # config #5 in fp64 (vs the fp64 restatement)
     ("casenml", 65536, 1, 8),          # config #2: replicated case.nml columns, fp64
+    ("conus", 524_288, 1, 4),          # config #4: one of 8 shards of the CONUS-like grid
 ])
 def test_full_size_sample_vs_oracle(engines, oracle_port, kind, ncol, opt_veg, precision):
     """BASELINE sizes: two steps of every column on the GPU, then a seeded
