@@ -34,7 +34,12 @@ FLAGS = ["-O3", f"--offload-arch={ARCH}", "-fPIC", "-shared", "-std=c++17",
          # MachineLICM hoists uniform offsets/constants out of the step and
          # Newton loops and holds them across the whole step: spills 70 -> 42
          # (single-step kernel) without it
-         "-mllvm", "-disable-machine-licm"]
+         "-mllvm", "-disable-machine-licm",
+         # no SLP vectorizer: the packed f32 ops it forms (v_pk_fma/mul/add,
+         # same IEEE result per element) need aligned register pairs; without
+         # them the fp32 step kernel spills 37 VGPRs instead of 52 (scratch
+         # 168 -> 124 B/lane) and config #3 runs +2.3 % (profiles/r02/noslp_ab.txt)
+         "-fno-slp-vectorize"]
 
 
 def source_hash(extra: tuple = (), source_flags: dict | None = None) -> str:

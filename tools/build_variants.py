@@ -76,6 +76,9 @@ VARIANTS = {
     "dvnoguard": ("-DNMP_F64_DV_NOGUARD",),
     "dvieee": ("-DNMP_F64_IEEE_DIV",),
     "ocmlpow": ("-DNMP_F64_OCML_POW",),
+    "noslp": ("-fno-slp-vectorize",),
+    "o2": ("-O2",),
+    "gcprio": ("-mllvm", "-greedy-regclass-priority-trumps-globalness=true"),
     # per-wave start/end records (tools/wave_timeline.py)
     "wt": ("-DNMP_WAVE_TIMING",),
     "wt_b128": ("-DNMP_WAVE_TIMING", "-DNMP_BLOCK=128", "-DNMP_PREFETCH=0"),
