@@ -39,7 +39,11 @@ FLAGS = ["-O3", f"--offload-arch={ARCH}", "-fPIC", "-shared", "-std=c++17",
          # same IEEE result per element) need aligned register pairs; without
          # them the fp32 step kernel spills 37 VGPRs instead of 52 (scratch
          # 168 -> 124 B/lane) and config #3 runs +2.3 % (profiles/r02/noslp_ab.txt)
-         "-fno-slp-vectorize"]
+         "-fno-slp-vectorize",
+         # no scalar partial-redundancy elimination (GVN-PRE): fewer values
+         # kept live across branches; config #3 +0.7 %, config #5 +1.3 %
+         # (profiles/r02/flags3_ab.txt)
+         "-mllvm", "-enable-pre=false"]
 
 
 def source_hash(extra: tuple = (), source_flags: dict | None = None) -> str:

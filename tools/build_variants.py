@@ -77,6 +77,13 @@ VARIANTS = {
     "dvieee": ("-DNMP_F64_IEEE_DIV",),
     "ocmlpow": ("-DNMP_F64_OCML_POW",),
     "noslp": ("-fno-slp-vectorize",),
+    "nolpre": ("-mllvm", "-enable-load-pre=false"),
+    "nopre": ("-mllvm", "-enable-pre=false"),
+    "nounroll": ("-fno-unroll-loops",),
+    "nopostmis": ("-mllvm", "-enable-post-misched=false"),
+    "nosink": ("-mllvm", "-simplifycfg-sink-common=false"),
+    "nohoist": ("-mllvm", "-simplifycfg-hoist-common=false"),
+    "phifold8": ("-mllvm", "-two-entry-phi-node-folding-threshold=8"),
     "o2": ("-O2",),
     "gcprio": ("-mllvm", "-greedy-regclass-priority-trumps-globalness=true"),
     # per-wave start/end records (tools/wave_timeline.py)

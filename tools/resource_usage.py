@@ -31,7 +31,7 @@ def main(extra):
     src = os.path.join(build.CSRC, "sflx_kernel.hip")
     with tempfile.TemporaryDirectory() as td:
         cmd = [build.HIPCC, "-O3", "--offload-arch=gfx950", "-std=c++17", "-ffp-contract=off",
-               "-mllvm", "-disable-machine-licm", "-fno-slp-vectorize", "-I", os.path.join(ROOT, "include"), "-I", build.CSRC,
+               "-mllvm", "-disable-machine-licm", "-fno-slp-vectorize", "-mllvm", "-enable-pre=false", "-I", os.path.join(ROOT, "include"), "-I", build.CSRC,
                "--offload-device-only", "-c", src, "-o", os.path.join(td, "k.o"),
                "-Rpass-analysis=kernel-resource-usage", *extra]
         out = subprocess.run(cmd, capture_output=True, text=True, check=True).stderr
