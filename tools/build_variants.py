@@ -84,6 +84,11 @@ VARIANTS = {
     "nosink": ("-mllvm", "-simplifycfg-sink-common=false"),
     "nohoist": ("-mllvm", "-simplifycfg-hoist-common=false"),
     "phifold8": ("-mllvm", "-two-entry-phi-node-folding-threshold=8"),
+    "exhaust": ("-mllvm", "-exhaustive-register-search"),
+    "defer": ("-mllvm", "-enable-deferred-spilling"),
+    "nomcse": ("-mllvm", "-disable-machine-cse"),
+    "notaildup": ("-mllvm", "-disable-tail-duplicate", "-mllvm", "-disable-early-taildup"),
+    "gvnsink": ("-mllvm", "-enable-gvn-sink"),
     "o2": ("-O2",),
     "gcprio": ("-mllvm", "-greedy-regclass-priority-trumps-globalness=true"),
     # per-wave start/end records (tools/wave_timeline.py)
