@@ -89,6 +89,7 @@ VARIANTS = {
     "nomcse": ("-mllvm", "-disable-machine-cse"),
     "notaildup": ("-mllvm", "-disable-tail-duplicate", "-mllvm", "-disable-early-taildup"),
     "gvnsink": ("-mllvm", "-enable-gvn-sink"),
+    "nolsv": ("-mllvm", "-amdgpu-load-store-vectorizer=false"),
     "o2": ("-O2",),
     "gcprio": ("-mllvm", "-greedy-regclass-priority-trumps-globalness=true"),
     # per-wave start/end records (tools/wave_timeline.py)
