@@ -26,7 +26,11 @@ HEADERS = ["dev_params.h", "sflx_kargs.h", "sflx_math.h", "sflx_routines.h", "gl
 # -freciprocal-math or -fapprox-func its divisions outside the Newton loops
 # become reciprocal sequences, which measured no faster on configs #2/#5
 # (profiles/r02/f64_flags_ab.txt), so it builds with the common flags.
-SOURCE_FLAGS = {"sflx_kernel.hip": ["-DNMP_TU=4"], "sflx_kernel_f64.hip": []}
+# fp32 translation unit: no SimplifyCFG sinking of instructions common to both
+# arms of a branch (config #3 +0.95 % over 4 interleaved A/B rounds; the fp64
+# kernels measured -1 % with it, profiles/r02/f32only_ab.txt)
+SOURCE_FLAGS = {"sflx_kernel.hip": ["-DNMP_TU=4", "-mllvm", "-simplifycfg-sink-common=false"],
+                "sflx_kernel_f64.hip": []}
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")
 FLAGS = ["-O3", f"--offload-arch={ARCH}", "-fPIC", "-shared", "-std=c++17",

@@ -90,6 +90,9 @@ VARIANTS = {
     "notaildup": ("-mllvm", "-disable-tail-duplicate", "-mllvm", "-disable-early-taildup"),
     "gvnsink": ("-mllvm", "-enable-gvn-sink"),
     "nolsv": ("-mllvm", "-amdgpu-load-store-vectorizer=false"),
+    # fp32 translation unit only
+    "notaildup32": {"f32": ["-mllvm", "-disable-tail-duplicate", "-mllvm", "-disable-early-taildup"]},
+    "nosink32": {"f32": ["-mllvm", "-simplifycfg-sink-common=false"]},
     "o2": ("-O2",),
     "gcprio": ("-mllvm", "-greedy-regclass-priority-trumps-globalness=true"),
     # per-wave start/end records (tools/wave_timeline.py)
@@ -108,6 +111,8 @@ if __name__ == "__main__":
             sf = dict(build.SOURCE_FLAGS)
             if "f64" in v:
                 sf["sflx_kernel_f64.hip"] = list(v["f64"])
+            if "f32" in v:  # extra flags for the fp32 translation unit only
+                sf["sflx_kernel.hip"] = list(sf["sflx_kernel.hip"]) + list(v["f32"])
             return build.build(force=True, verbose=False, out=os.path.join(vdir, f"lib_{n}.so"),
                                extra=tuple(v.get("extra", ())), source_flags=sf)
         return build.build(force=True, verbose=False, out=os.path.join(vdir, f"lib_{n}.so"), extra=v)
