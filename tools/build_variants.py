@@ -93,6 +93,8 @@ VARIANTS = {
     # fp32 translation unit only
     "notaildup32": {"f32": ["-mllvm", "-disable-tail-duplicate", "-mllvm", "-disable-early-taildup"]},
     "nosink32": {"f32": ["-mllvm", "-simplifycfg-sink-common=false"]},
+    "phifold1_32": {"f32": ["-mllvm", "-two-entry-phi-node-folding-threshold=1"]},
+    "specoff32": {"f32": ["-mllvm", "-speculate-one-expensive-inst=false"]},
     "o2": ("-O2",),
     "gcprio": ("-mllvm", "-greedy-regclass-priority-trumps-globalness=true"),
     # per-wave start/end records (tools/wave_timeline.py)
