@@ -13,9 +13,13 @@ every column (one kernel launch, state resident in HBM); every
 gathers them to rank 0, the writing rank (RCCL over xGMI, --gather root; or
 all-gathers them to every rank with --gather all) on a side stream.
 
-Multi-GPU: one process per GPU (torchrun), columns statically sharded with
-no data-path collective other than that diagnostics gather; per-GPU work
-is fixed (weak scaling).
+Multi-GPU: one process per GPU, columns statically sharded with no data-path
+collective other than that diagnostics gather; per-GPU work is fixed (weak
+scaling).  `--gpus N` under torchrun (WORLD_SIZE = N) runs as that launcher's
+rank; without a launcher bench.py starts the N rank processes itself
+(`spawn_ranks`, before anything touches the GPU) and exits non-zero if any
+rank fails or WORLD_SIZE disagrees with --gpus -- it never measures one GPU
+under an N-GPU label.
 
 Prints one JSON line (rank 0) with the driver contract fields plus
 `roofline` (dominant kernel vs HBM peak) and `cpu_baseline`.
@@ -41,6 +45,41 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E, /opt/skills/guides/MI355X_MICROARCH.md
 # (MI355X_MICROARCH.md, "Wave scheduling"; f64 and transcendental instructions take
 # longer, so the fraction below is a lower bound on the VALU pipe's busy share)
 VALU_PEAK_GINST = 256 * 4 * 2.4 / 2
+SIMDS, CLOCK_GHZ = 256 * 4, 2.39  # the kernel holds 2.39 GHz (profiles/r02/clock.txt)
+# SIMD cycles per wave64 VALU instruction by class (MI355X_MICROARCH.md constants
+# table: v_fma_f32 2 cyc on a SIMD-32; the vector fp64 rate is half the fp32 rate;
+# v_exp/v_log/v_rcp/v_sqrt issue at a quarter of the fp32 rate); every other VALU
+# instruction (moves, selects, compares, integer, conversions) at the fp32 rate
+VALU_CYCLES = {"f32": 2, "f64": 4, "trans_f32": 8, "trans_f64": 16, "other": 2}
+
+
+def valu_weighted(tj: dict, launches: int, step_ms: float):
+    """Cycle-weighted VALU busy share of the chip: sum over
+    the instruction classes of (count x SIMD cycles per wave64 instruction),
+    per step, over (SIMDs x clock x GPU step time).  Counts from the PMC
+    passes in profiles/traffic.json (per dispatch)."""
+    k = ("SQ_INSTS_VALU", "SQ_INSTS_VALU_ADD_F32", "SQ_INSTS_VALU_MUL_F32",
+         "SQ_INSTS_VALU_FMA_F32", "SQ_INSTS_VALU_TRANS_F32", "SQ_INSTS_VALU_ADD_F64",
+         "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_FMA_F64")
+    if not all(x in tj for x in k):
+        return None
+    f32 = sum(tj[f"SQ_INSTS_VALU_{o}_F32"] for o in ("ADD", "MUL", "FMA"))
+    f64 = sum(tj[f"SQ_INSTS_VALU_{o}_F64"] for o in ("ADD", "MUL", "FMA"))
+    t32, t64 = tj["SQ_INSTS_VALU_TRANS_F32"], tj.get("SQ_INSTS_VALU_TRANS_F64", 0.0)
+    other = tj["SQ_INSTS_VALU"] - f32 - f64 - t32 - t64
+    cls = {"f32": f32, "f64": f64, "trans_f32": t32, "trans_f64": t64, "other": other}
+    cyc = sum(cls[c] * VALU_CYCLES[c] for c in cls) * launches
+    avail = SIMDS * CLOCK_GHZ * 1e9 * step_ms * 1e-3
+    out = {"weighted": cyc / avail, "cycles_per_class": VALU_CYCLES,
+           "insts_per_wave": {c: v / tj["SQ_WAVES"] for c, v in cls.items()},
+           "simd_cycles_per_step": cyc, "simd_cycles_available": avail}
+    if "SQ_ACTIVE_INST_VALU" in tj:
+        # quad-cycles (MI355X_MICROARCH.md: SQ_ACTIVE_INST_* count quad-cycles),
+        # summed over waves: overlapping waves count separately, so it can
+        # exceed the SIMDs' cycles -- reported raw, not as a pipe share
+        out["active_inst_valu_per_simd_cycle"] = (4 * tj["SQ_ACTIVE_INST_VALU"] * launches
+                                                  / avail)
+    return out
 METRIC = BASELINE_METRIC = "land-columns·timesteps/sec at 4 soil + 3 snow layers, 1/2/4/8 MI355X"
 
 
@@ -116,19 +155,106 @@ def parse():
                          "choice (fewer per wave when the column set cannot fill the chip)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-steps", type=int, default=32)
+    ap.add_argument("--launch-probe", action="store_true",
+                    help="launcher check only (CPU tests): every rank joins the process group "
+                         "over gloo and contributes its column count, rank 0 prints the line "
+                         "with n_gpus and the summed columns; no GPU is touched, no rate")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic.json"),
                     help="PMC-measured HBM bytes per launch (written by tools/pmc_traffic.py)")
     return ap.parse_args()
 
 
+def _free_port() -> int:
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(n: int, check_gpus: bool = True) -> int:
+    """`bench.py --gpus N` started without a launcher: start N rank processes
+    of this same command (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set, one
+    per GPU, rendezvous on 127.0.0.1) and return the job's exit status.  This
+    process never touches the GPU (it only counts devices), so the ranks are
+    children, not an exec.  Any rank failing fails the job: the others are
+    stopped and the status is non-zero -- never a silent one-GPU line."""
+    import signal
+    import subprocess
+    backend = os.environ.get("NMP_BENCH_BACKEND", "nccl")
+    if backend == "nccl" and check_gpus:
+        import torch  # device_count() does not initialise the GPU on this image
+        have = torch.cuda.device_count()
+        if have < n:
+            print(f"bench.py: --gpus {n} needs {n} visible GPUs for RCCL, {have} found",
+                  file=sys.stderr, flush=True)
+            return 2
+    port = os.environ.get("MASTER_PORT") or str(_free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=port,
+                   NMP_BENCH_SPAWNED="1")
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *sys.argv[1:]],
+                                      env=env, start_new_session=True))
+    status = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            rc = p.poll()
+            if rc is None:
+                continue
+            live.remove(p)
+            if rc != 0 and status == 0:
+                status = rc if rc > 0 else 128 - rc
+                print(f"bench.py: rank {procs.index(p)} exited with {rc}; stopping the job",
+                      file=sys.stderr, flush=True)
+                for q in live:  # a rank blocked in a collective would wait forever
+                    try:
+                        os.killpg(q.pid, signal.SIGTERM)
+                    except ProcessLookupError:
+                        pass
+        time.sleep(0.05)
+    return status
+
+
+def launch_probe(a, world: int, rank: int, use_dist: bool):
+    """--launch-probe: the rank layout and rendezvous of a run, without the GPU.
+    Each rank builds its column block (the same generator call as a run) and the
+    ranks all-reduce (count, first global column index) over gloo."""
+    import torch
+    import torch.distributed as dist
+    from noahmp_amd.params import Params
+    cols = cases.make_columns(a.ncol, a.kind, Params.builtin("STAS", "USGS").as_dict(),
+                              seed=1000 + rank, julian=180.0, first=rank * a.ncol)
+    t = torch.tensor([cols.isnow.shape[0], rank * a.ncol, 1], dtype=torch.int64)
+    if use_dist:
+        dist.init_process_group("gloo")
+        dist.all_reduce(t)
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "value": None, "unit": "column-steps/s",
+                          "n_gpus": world, "launch_probe": True, "ranks_joined": int(t[2]),
+                          "ncol_total": int(t[0]), "first_col_sum": int(t[1])}), flush=True)
+    if use_dist:
+        dist.destroy_process_group()
+
+
 def main():
     a = parse()
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(a.gpus, check_gpus=not a.launch_probe))
     world = int(os.environ.get("WORLD_SIZE", "1"))
-    # launched by torchrun (even with one rank): take the distributed path
+    # launched by torchrun or spawn_ranks (even with one rank): the distributed path
     use_dist = "RANK" in os.environ and "MASTER_ADDR" in os.environ
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    assert world == a.gpus or world == 1, "launch N>1 with torchrun --nproc-per-node N"
+    if world != a.gpus:
+        print(f"bench.py: --gpus {a.gpus} but WORLD_SIZE {world}: launch with torchrun "
+              f"--nproc-per-node {a.gpus}, or without a launcher", file=sys.stderr, flush=True)
+        sys.exit(2)
+    if os.environ.get("NMP_BENCH_FAIL_RANK") == str(rank):  # test hook: a rank that dies
+        sys.exit(3)
+    if a.launch_probe:
+        return launch_probe(a, world, rank, use_dist)
 
     from noahmp_amd.params import Params
     P = Params.builtin("STAS", "USGS")
@@ -281,6 +407,9 @@ def main():
                             "insts_per_wave": tj["SQ_INSTS_VALU"] / tj["SQ_WAVES"],
                             "source": "SQ_INSTS_VALU / SQ_WAVES, rocprofv3 --pmc "
                                       "(profiles/traffic.json)"}
+                    w = valu_weighted(tj, len(ranges.ranges), step_ms)
+                    if w is not None:
+                        valu.update(w)
         line = {
             "metric": METRIC, "value": value, "unit": "column-steps/s", "n_gpus": world,
             "steps": a.steps, "warmup": a.warmup, "ms_per_step": elapsed * 1e3 / a.steps,

@@ -20,6 +20,8 @@
  *                             stops after the namelist): many steps, one launch
  * nmp_sflx_columns,           noahmp_sflx itself, argument for argument, on n host records
  *   nmp_sflx_column                                         core/module_noahmp_func.f90:66-476
+ * nmp_frh2o, nmp_frh2o_host   frh2o (public routine)        core/module_noahmp_func.f90:4494-4598
+ * nmp_calhum, nmp_calhum_host calhum (public by default)     core/module_noahmp_func.f90:3958-3984
  * nmp_state_from_aos          layout bridge from noahmp_state_t records
  *                                                           core/module_noahmp_type.f90:10-42
  * nmp_finalize, nmp_strerror  (error path of utils `assert`/`stop`, core/module_noahmp_utils.f90:21-53)
@@ -52,7 +54,7 @@
 extern "C" {
 #endif
 
-#define NMP_ABI_VERSION 3
+#define NMP_ABI_VERSION 4
 
 /* ---- dimensions (core/module_noahmp_global.f90:9-13) -------------------- */
 #define NMP_NSOIL 4
@@ -333,6 +335,32 @@ int nmp_state_from_aos(const void* records, int64_t n, int64_t ld, float* state,
  *    have called wrf_error_fatal / wrf_message). */
 int nmp_sflx_columns(nmp_engine* eng, nmp_sflx_args* cols, int64_t n);
 int nmp_sflx_column(nmp_engine* eng, nmp_sflx_args* col);
+
+/* The reference's other public physics routines, batched: element i is one
+ * `call frh2o(sltyp(i), FREE(i), TKELV(i), SMC(i), soilwat(i))`
+ * (core/module_noahmp_func.f90:4494-4598; public at :6-8) or one
+ * `call calhum(SFCTMP(i), SFCPRS(i), Q2SAT(i), DQSDT2(i))` (:3958-3984; a
+ * module procedure, public by default).  Reals are the engine's precision;
+ * frh2o reads LK_BEXP / LK_PSISAT / LK_SMCMAX of the soil type from the
+ * engine's tables, as the reference reads its module arrays.  The device code
+ * is the one noahmp_sflx inlines, so in the fp32 "ref" math policy the values
+ * are the reference's bit for bit.
+ *  - nmp_frh2o / nmp_calhum: device pointers, enqueued on `stream`.
+ *  - nmp_frh2o_host / nmp_calhum_host: host arrays, synchronous (copy in,
+ *    launch, copy out) -- the drop-in for the scalar Fortran calls (n = 1).
+ *  - frh2o: col_status (may be NULL) is OR-ed with NMP_ST_FLERCH where the
+ *    reference would call wrf_message (Flerchinger fallback, :4586-4590), and
+ *    with NMP_ST_STOP for a soil type outside 1..NMP_MSLTYP (FREE = NaN).
+ *  - calhum: q2sat or dqsdt2 may be NULL (not computed). */
+int nmp_frh2o(nmp_engine* eng, int64_t n, const int32_t* sltyp, const void* tkelv,
+              const void* smc, const void* soilwat, void* free_water, int32_t* col_status,
+              void* stream);
+int nmp_frh2o_host(nmp_engine* eng, int64_t n, const int32_t* sltyp, const void* tkelv,
+                   const void* smc, const void* soilwat, void* free_water, int32_t* col_status);
+int nmp_calhum(nmp_engine* eng, int64_t n, const void* sfctmp, const void* sfcprs, void* q2sat,
+               void* dqsdt2, void* stream);
+int nmp_calhum_host(nmp_engine* eng, int64_t n, const void* sfctmp, const void* sfcprs,
+                    void* q2sat, void* dqsdt2);
 
 /* Transcendental policy for fp32 engines: 0 = "ref", a bit-exact restatement of
  * the glibc float libm the reference is linked against (csrc/glibc_math.h;

@@ -470,6 +470,17 @@ struct SflxPack {
 };
 static_assert(NMP_NSTATE - NMP_S_TV == 28, "scalar state block");
 
+// one device allocation freed on scope exit (the synchronous host entries)
+struct DevBlock {
+  void* p = nullptr;
+  char* alloc(size_t nb) {
+    return hipMalloc(&p, nb) == hipSuccess ? static_cast<char*>(p) : (p = nullptr, nullptr);
+  }
+  ~DevBlock() {
+    if (p) (void)hipFree(p);
+  }
+};
+
 bool same_f(float a, float b) { return std::memcmp(&a, &b, sizeof(float)) == 0; }
 
 template <class T>
@@ -541,6 +552,86 @@ int nmp_sflx_columns(nmp_engine* eng, nmp_sflx_args* cols, int64_t n) {
 }
 
 int nmp_sflx_column(nmp_engine* eng, nmp_sflx_args* col) { return nmp_sflx_columns(eng, col, 1); }
+
+int nmp_frh2o(nmp_engine* eng, int64_t n, const int32_t* sltyp, const void* tkelv,
+              const void* smc, const void* soilwat, void* free_water, int32_t* col_status,
+              void* stream) {
+  if (!eng || n < 0) return NMP_E_ARG;
+  if (n == 0) return NMP_OK;
+  if (!sltyp || !tkelv || !smc || !soilwat || !free_water) return NMP_E_ARG;
+  if (ensure_device(eng->device) != NMP_OK) return NMP_E_DEVICE;
+  return nmp::launch_frh2o(eng->precision, eng->math, eng->dparams, n, sltyp, tkelv, smc, soilwat,
+                           free_water, col_status, static_cast<hipStream_t>(stream)) == hipSuccess
+             ? NMP_OK
+             : NMP_E_DEVICE;
+}
+
+int nmp_calhum(nmp_engine* eng, int64_t n, const void* sfctmp, const void* sfcprs, void* q2sat,
+               void* dqsdt2, void* stream) {
+  if (!eng || n < 0) return NMP_E_ARG;
+  if (n == 0) return NMP_OK;
+  if (!sfctmp || !sfcprs) return NMP_E_ARG;
+  if (ensure_device(eng->device) != NMP_OK) return NMP_E_DEVICE;
+  return nmp::launch_calhum(eng->precision, eng->math, n, sfctmp, sfcprs, q2sat, dqsdt2,
+                            static_cast<hipStream_t>(stream)) == hipSuccess
+             ? NMP_OK
+             : NMP_E_DEVICE;
+}
+
+int nmp_frh2o_host(nmp_engine* eng, int64_t n, const int32_t* sltyp, const void* tkelv,
+                   const void* smc, const void* soilwat, void* free_water, int32_t* col_status) {
+  if (!eng || n < 0) return NMP_E_ARG;
+  if (n == 0) return NMP_OK;
+  if (!sltyp || !tkelv || !smc || !soilwat || !free_water) return NMP_E_ARG;
+  if (ensure_device(eng->device) != NMP_OK) return NMP_E_DEVICE;
+  const size_t nr = (size_t)n * eng->precision, ni = (size_t)n * sizeof(int32_t);
+  DevBlock d;
+  char* base = d.alloc(4 * nr + 2 * ni);
+  if (!base) return NMP_E_DEVICE;
+  char *t = base, *m = t + nr, *w = m + nr, *o = w + nr;
+  int32_t* s = reinterpret_cast<int32_t*>(o + nr);
+  int32_t* st = s + n;
+  if (hipMemcpy(t, tkelv, nr, hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(m, smc, nr, hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(w, soilwat, nr, hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(s, sltyp, ni, hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemset(st, 0, ni) != hipSuccess)
+    return NMP_E_DEVICE;
+  if (nmp::launch_frh2o(eng->precision, eng->math, eng->dparams, n, s, t, m, w, o, st, nullptr) !=
+          hipSuccess ||
+      hipDeviceSynchronize() != hipSuccess ||
+      hipMemcpy(free_water, o, nr, hipMemcpyDeviceToHost) != hipSuccess)
+    return NMP_E_DEVICE;
+  if (col_status) {
+    std::vector<int32_t> bits(n);
+    if (hipMemcpy(bits.data(), st, ni, hipMemcpyDeviceToHost) != hipSuccess) return NMP_E_DEVICE;
+    for (int64_t i = 0; i < n; ++i) col_status[i] |= bits[i];
+  }
+  return NMP_OK;
+}
+
+int nmp_calhum_host(nmp_engine* eng, int64_t n, const void* sfctmp, const void* sfcprs,
+                    void* q2sat, void* dqsdt2) {
+  if (!eng || n < 0) return NMP_E_ARG;
+  if (n == 0) return NMP_OK;
+  if (!sfctmp || !sfcprs) return NMP_E_ARG;
+  if (ensure_device(eng->device) != NMP_OK) return NMP_E_DEVICE;
+  const size_t nr = (size_t)n * eng->precision;
+  DevBlock d;
+  char* base = d.alloc(4 * nr);
+  if (!base) return NMP_E_DEVICE;
+  char *t = base, *p = t + nr, *q = p + nr, *dq = q + nr;
+  if (hipMemcpy(t, sfctmp, nr, hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(p, sfcprs, nr, hipMemcpyHostToDevice) != hipSuccess)
+    return NMP_E_DEVICE;
+  if (nmp::launch_calhum(eng->precision, eng->math, n, t, p, q2sat ? q : nullptr,
+                         dqsdt2 ? dq : nullptr, nullptr) != hipSuccess ||
+      hipDeviceSynchronize() != hipSuccess ||
+      (q2sat && hipMemcpy(q2sat, q, nr, hipMemcpyDeviceToHost) != hipSuccess) ||
+      (dqsdt2 && hipMemcpy(dqsdt2, dq, nr, hipMemcpyDeviceToHost) != hipSuccess))
+    return NMP_E_DEVICE;
+  return NMP_OK;
+}
 
 void nmp_finalize(nmp_engine* eng) {
   if (!eng) return;

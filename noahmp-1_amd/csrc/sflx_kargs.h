@@ -58,6 +58,14 @@ hipError_t launch_forcing_synth(int precision, int64_t ncol, int64_t ld, const v
                                 double julian, int32_t yearlen, uint64_t seed, int64_t step,
                                 int64_t first_col, void* out, hipStream_t stream);
 
+// csrc/routines.hip: the reference's public routines frh2o / calhum over n
+// elements (device pointers, engine precision; math 0 = the fp32 "ref" policy)
+hipError_t launch_frh2o(int precision, int math, const DevParams* P, int64_t n,
+                        const int32_t* sltyp, const void* tkelv, const void* smc, const void* sh2o,
+                        void* out, int32_t* status, hipStream_t stream);
+hipError_t launch_calhum(int precision, int math, int64_t n, const void* sfctmp,
+                         const void* sfcprs, void* q2sat, void* dqsdt2, hipStream_t stream);
+
 // csrc/rebin.hip: per-tile counting sort of the columns by cost key
 hipError_t launch_rebin(const uint8_t* cost, int32_t* order, int64_t ncol, int tile,
                         hipStream_t stream);

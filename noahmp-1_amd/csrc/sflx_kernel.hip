@@ -373,9 +373,30 @@ DEV void sfcdif2(int iter, T z0, T thz0, T thlm, T sfcspd, T czil, T zlm, T& akm
 }
 
 // ragrb: func.f90:3260-3350
+// Optional value dump of one column (build with -DNMP_DEBUG_DUMP; tools only,
+// tools/mcse_probe.py): NMP_DBG(i, v) stores v into nmp_dbg[i] when the lane
+// steps column nmp_dbg_col.  Compiled out otherwise.
+#ifdef NMP_DEBUG_DUMP
+static __device__ double nmp_dbg[256];
+static __device__ long long nmp_dbg_col = -1;
+#define NMP_DBG_ARG , bool dbg_lane
+#define NMP_DBG_PASS , dbg_lane
+#else
+#define NMP_DBG_ARG
+#define NMP_DBG_PASS
+#endif
+#ifdef NMP_DEBUG_DUMP
+#define NMP_DBG(i, v)                        \
+  do {                                       \
+    if (dbg_lane) nmp_dbg[i] = (double)(v);  \
+  } while (0)
+#else
+#define NMP_DBG(i, v) ((void)0)
+#endif
+
 template <class T, bool R>
 DEV void ragrb(T sqrt_dleaf_uc, int iter, T vai, T rhoair, T hg, T tah, T zpd, T z0mg, T z0hg,
-               T hcan, T z0h, T fv, T cwp, T mpe, T& fhg, T& rahg, T& rb) {
+               T hcan, T z0h, T fv, T cwp, T mpe, T& fhg, T& rahg, T& rb NMP_DBG_ARG) {
   typedef Mth<T, R> M;
   T mozg = L(0.0);
   if (iter > 1) {
@@ -394,6 +415,12 @@ DEV void ragrb(T sqrt_dleaf_uc, int iter, T vai, T rhoair, T hg, T tah, T zpd, T
   rahg = dv(tmprah2, kh);
   T tmprb = dv(cwpc * L(50.0), L(1.0) - M::exp(-cwpc / L(2.0)));
   rb = tmprb * sqrt_dleaf_uc;
+  if (iter == 1) {
+    NMP_DBG(208, hcan); NMP_DBG(209, zpd); NMP_DBG(210, z0mg); NMP_DBG(211, z0h);
+    NMP_DBG(212, fv); NMP_DBG(213, vai); NMP_DBG(214, cwp); NMP_DBG(215, cwpc);
+    NMP_DBG(216, tmp1); NMP_DBG(217, tmp2); NMP_DBG(218, tmprah2); NMP_DBG(219, kh);
+    NMP_DBG(220, rahg); NMP_DBG(221, tmprb); NMP_DBG(222, fhg); NMP_DBG(223, z0hg);
+  }
 }
 
 // stomata (Ball-Berry bisection): func.f90:3739-3887
@@ -484,14 +511,8 @@ DEV void canres(const VegRec& V, T sfcprs, T tv, T par, T eah, T btran, T& rs, T
   typedef Mth<T, R> M;
   T q2 = L(0.622) * eah / (sfcprs - L(0.378) * eah);
   q2 = q2 / (L(1.0) + q2);
-  const T A2 = L(17.67), A3 = L(273.15), A4 = L(29.65), ELWV = L(2.501E6);
-  const T A23M4 = A2 * (A3 - A4), E0 = L(0.611), RV = L(461.0), EPS = L(0.622);
-  T es = E0 * M::exp(ELWV / RV * (L(1.) / A3 - L(1.) / tv));
-  T sfcprsx = sfcprs * L(1.E-3);
-  T q2sat = EPS * es / (sfcprsx - es);
-  q2sat = q2sat * L(1.E3);
-  q2sat = q2sat / L(1.E3);
-  (void)A23M4;
+  T q2sat, dqsdt2;  // (DQSDT2 unused by canres: the compiler drops it)
+  calhum<T, R>(tv, sfcprs, q2sat, dqsdt2);
   T ff = L(2.0) * par / (T)V.rgl;
   T rcs = (ff + (T)V.rsmin / (T)V.rsmax) / (L(1.0) + ff);
   rcs = rmin(rmax(rcs, L(0.0001)), L(1.0));
@@ -835,12 +856,19 @@ struct Sink {
 // not held through the loops, DESIGN.md "Layer state across the flux loops").
 // Layout [field][thread] (28 x NMP_BLOCK floats, 28 KB per 256-thread block:
 // with the 11.5 KB of tables four blocks still fit a CU's 160 KB).  Each lane
-// reads back only its own slots, which its own copy wrote, so no barrier is
-// needed; nothing writes these fields before the second read.  (Issuing the
+// reads back only its own slots, which its own wave's copy wrote, so no
+// workgroup barrier is needed, only the wave's own wait for the DMA (an
+// explicit s_waitcnt vmcnt(0) before the first read); nothing writes these
+// fields before the second read.  (Issuing the
 // copy later, as a prefetch before the flux loops, does not hide its latency:
 // vmcnt counts in order, so the first spill reload after it waits for it.)
 #ifndef NMP_PREFETCH
 #define NMP_PREFETCH 3
+#endif
+// explicit wait for the copy before its first read (tuning A/B only: 0 leaves
+// the wait to the compiler's LDS-DMA alias tracking, as round 2 did)
+#ifndef NMP_LDS_EXPLICIT_WAIT
+#define NMP_LDS_EXPLICIT_WAIT 1
 #endif
 constexpr int kPrefetchFields = NMP_S_SMC + 4;
 static_assert(NMP_S_STC == 0 && NMP_S_ZSNSO == 7 && NMP_S_SNICE == 14 && NMP_S_SNLIQ == 17 &&
@@ -933,6 +961,9 @@ constexpr Opt kOptionSet[3] = {{1, 1, 1, 1, 1, 1, 1, 1, 2, 1, 1, 1},
 template <class T, bool R, int OS>
 DEV void sflx_column(const DevParams& P, const KArgs<T>& A, Col<T>& c, const Sink<T>& out) {
   typedef Mth<T, R> M;
+#ifdef NMP_DEBUG_DUMP
+  const bool dbg_lane = (long long)(out.st - A.state) == nmp_dbg_col;
+#endif
 #ifdef NMP_PHASE_TIMING
   PhaseClock pclk{__builtin_amdgcn_s_memtime(), 0};
 #endif
@@ -1323,14 +1354,20 @@ DEV void sflx_column(const DevParams& P, const KArgs<T>& A, Col<T>& c, const Sin
           chv = chv / ur;
           cmv = cmv / ur;
         }
+        const int dbi = (iter <= 3 ? iter - 1 : 3) * 40;
+        NMP_DBG(dbi + 0, moz); NMP_DBG(dbi + 1, fm); NMP_DBG(dbi + 2, fh);
+        NMP_DBG(dbi + 3, cmv); NMP_DBG(dbi + 4, chv); NMP_DBG(dbi + 5, fv);
         rahc = rmax(L(1.0), dv(L(1.0), chv * ur));
+        NMP_DBG(dbi + 6, rahc);
         T rawc = rahc;
         ragrb<T, R>(sqrt_dleaf_uc, iter, vaie, rhoair, hg, c.tah, zpd, z0mg, z0mg, hcan, z0h, fv,
-                    cwp, mpe, fhg, rahg, rb);
+                    cwp, mpe, fhg, rahg, rb NMP_DBG_PASS);
+        NMP_DBG(dbi + 7, fhg); NMP_DBG(dbi + 8, rahg); NMP_DBG(dbi + 9, rb);
         T rawg = rahg;
         tt = tdc(c.tv);
         T estv, destv;
         esat_sel(tt, estv, destv);
+        NMP_DBG(dbi + 10, estv); NMP_DBG(dbi + 11, destv);
         if constexpr (decltype(first)::value) {  // iter == 1
           if (o.crs == 1) {
             const StomataPre<T> sp =
@@ -1360,6 +1397,11 @@ DEV void sflx_column(const DevParams& P, const KArgs<T>& A, Col<T>& c, const Sin
         T bea = dv(cew + ctw, cond);
         T cev = dv((L(1.0) - bea) * cew * rhoair * CPAIR, gammav);
         T ctr = dv((L(1.0) - bea) * ctw * rhoair * CPAIR, gammav);
+        NMP_DBG(dbi + 12, cah); NMP_DBG(dbi + 13, cvh); NMP_DBG(dbi + 14, cgh);
+        NMP_DBG(dbi + 15, ata); NMP_DBG(dbi + 16, bta); NMP_DBG(dbi + 17, caw);
+        NMP_DBG(dbi + 18, cew); NMP_DBG(dbi + 19, ctw); NMP_DBG(dbi + 20, cgw);
+        NMP_DBG(dbi + 21, aea); NMP_DBG(dbi + 22, bea); NMP_DBG(dbi + 23, cev);
+        NMP_DBG(dbi + 24, ctr); NMP_DBG(dbi + 25, rssun); NMP_DBG(dbi + 26, rssha);
         c.tah = ata + bta * c.tv;
         c.eah = aea + bea * estv;
         irc = fveg * (air + cir * p4(c.tv));
@@ -1381,6 +1423,11 @@ DEV void sflx_column(const DevParams& P, const KArgs<T>& A, Col<T>& c, const Sin
         h = dv(rhoair * CPAIR * (c.tah - c.sfctmp), rahc);
         hg = dv(rhoair * CPAIR * (tgv - c.tah), rahg);
         c.qsfc = dv(L(0.622) * c.eah, c.sfcprs - L(0.378) * c.eah);
+        NMP_DBG(dbi + 27, c.tah); NMP_DBG(dbi + 28, c.eah); NMP_DBG(dbi + 29, irc);
+        NMP_DBG(dbi + 30, shc); NMP_DBG(dbi + 31, evc); NMP_DBG(dbi + 32, tr);
+        NMP_DBG(dbi + 33, dtv); NMP_DBG(dbi + 34, c.tv); NMP_DBG(dbi + 35, h);
+        NMP_DBG(dbi + 36, hg); NMP_DBG(dbi + 37, c.qsfc); NMP_DBG(dbi + 38, sav);
+        NMP_DBG(dbi + 39, a);
         return dtv;
     };
     vtrips = 1;
@@ -1407,7 +1454,7 @@ DEV void sflx_column(const DevParams& P, const KArgs<T>& A, Col<T>& c, const Sin
       rahc = rmax(L(1.0), L(1.0) / (chv * ur));
       T rawc = rahc;
       ragrb<T, R>(sqrt_dleaf_uc, iter, vaie, rhoair, hg, c.tah, zpd, z0mg, z0mg, hcan, z0h, fv,
-                  cwp, mpe, fhg, rahg, rb);
+                  cwp, mpe, fhg, rahg, rb NMP_DBG_PASS);
       T rawg = rahg;
       tt = tdc(c.tv);
       T estv, destv;
@@ -2529,7 +2576,21 @@ NMP_UNROLL(kBareUnroll)
         pp[k] = L(0.);
         del[k] = L(0.);
       }
+      if (it == 1) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          NMP_DBG(160 + k, wdf[k]); NMP_DBG(164 + k, wcnd[k]); NMP_DBG(168 + k, ai[k]);
+          NMP_DBG(172 + k, bi[k]); NMP_DBG(176 + k, ci[k]); NMP_DBG(180 + k, rhstt[k]);
+          NMP_DBG(184 + k, c.sh2o[k]); NMP_DBG(188 + k, etrani[k]); NMP_DBG(196 + k, c.smc[k]);
+        }
+        NMP_DBG(200, qinfil); NMP_DBG(201, qseva); NMP_DBG(202, qinsrf); NMP_DBG(203, dtfine);
+        NMP_DBG(204, (T)niter); NMP_DBG(205, smcmax); NMP_DBG(206, bexp); NMP_DBG(207, dwsat);
+      }
       rosr12<T, 4>(pp, ai, bi, ciin, rin, del, 0);
+      if (it == 1) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) NMP_DBG(192 + k, pp[k]);
+      }
 #pragma unroll
       for (int k = 0; k < 4; ++k) c.sh2o[k] = c.sh2o[k] + pp[k];
       T wplus = L(0.0);
@@ -2853,9 +2914,37 @@ void sflx_step_kernel(const DevParams* __restrict__ gparams,
   const int64_t ld = a.ld;
   Col<T> c;
   const T* st = a.state + c0;
+  // layer state: through the LDS copy (kPrefetch) or straight from HBM.  The
+  // copy is issued first; the column's other fields load while it is in flight
+  if constexpr (kPrefetch<T, R>) copy_layers_to_lds(st, ld);
+  c.tv = gld(st + NMP_S_TV * ld); c.tg = gld(st + NMP_S_TG * ld);
+  c.fwet = gld(st + NMP_S_FWET * ld); c.snowh = gld(st + NMP_S_SNOWH * ld);
+  c.sneqv = gld(st + NMP_S_SNEQV * ld);
+  c.lai = gld(st + NMP_S_LAI * ld); c.sai = gld(st + NMP_S_SAI * ld);
+  // ALBOLD/TAUSS/QSNOW/SNEQVO: loaded where used (daylight radiation block);
+  // QSNOW and SNEQVO are reassigned before the water phase reads them
+  c.albold = c.tauss = c.qsnow = c.sneqvo = (T)0;
+  c.isnow = gld(a.isnow + c0);
+  const T* sf = a.static_f + c0;
+  c.lat = gld(sf + NMP_F_LAT * ld); c.zref = gld(sf + NMP_F_ZLVL * ld); c.shdfac = gld(sf + NMP_F_SHDFAC * ld);
+  c.shdmax = gld(sf + NMP_F_SHDMAX * ld);
+  const int32_t* si = a.static_i + c0;
+  c.lutyp = gld(si + NMP_I_VEGTYP * ld); c.sltyp = gld(si + NMP_I_SOILTYP * ld);
+  c.isc = gld(si + NMP_I_SOILCOLOR * ld);
+  c.ist = gld(si + NMP_I_IST * ld); c.ice = gld(si + NMP_I_ICE * ld);
+  const T* fc = a.forcing + c0;
+  c.sfctmp = gld(fc + NMP_A_SFCTMP * ld); c.sfcprs = gld(fc + NMP_A_SFCPRS * ld); c.psfc = gld(fc + NMP_A_PSFC * ld);
+  c.uu = gld(fc + NMP_A_UU * ld); c.vv = gld(fc + NMP_A_VV * ld); c.q2 = gld(fc + NMP_A_Q2 * ld);
+  c.soldn = gld(fc + NMP_A_SOLDN * ld); c.lwdn = gld(fc + NMP_A_LWDN * ld);
+  c.cosz = gld(fc + NMP_A_COSZ * ld);
+  c.status = 0;
   {
-    // layer state: through the LDS copy (kPrefetch) or straight from HBM
-    if constexpr (kPrefetch<T, R>) copy_layers_to_lds(st, ld);
+    // the copy's completion is explicit: LDS-DMA loads count in vmcnt, and
+    // the "memory" clobber keeps every LDS read of the copied fields (here and
+    // the re-read after the flux loops, Sink::fresh_state) below the wait
+#if NMP_LDS_EXPLICIT_WAIT
+    if constexpr (kPrefetch<T, R>) __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
     auto rd = [&](int f) -> T {
       if constexpr (kPfEntry<T, R>)
         return lds_pool()[f * NMP_BLOCK + threadIdx.x];
@@ -2878,27 +2967,6 @@ void sflx_step_kernel(const DevParams* __restrict__ gparams,
       c.smc[k] = rd(NMP_S_SMC + k);
     }
   }
-  c.tv = gld(st + NMP_S_TV * ld); c.tg = gld(st + NMP_S_TG * ld);
-  c.fwet = gld(st + NMP_S_FWET * ld); c.snowh = gld(st + NMP_S_SNOWH * ld);
-  c.sneqv = gld(st + NMP_S_SNEQV * ld);
-  c.lai = gld(st + NMP_S_LAI * ld); c.sai = gld(st + NMP_S_SAI * ld);
-  // ALBOLD/TAUSS/QSNOW/SNEQVO: loaded where used (daylight radiation block);
-  // QSNOW and SNEQVO are reassigned before the water phase reads them
-  c.albold = c.tauss = c.qsnow = c.sneqvo = (T)0;
-  c.isnow = gld(a.isnow + c0);
-  const T* sf = a.static_f + c0;
-  c.lat = gld(sf + NMP_F_LAT * ld); c.zref = gld(sf + NMP_F_ZLVL * ld); c.shdfac = gld(sf + NMP_F_SHDFAC * ld);
-  c.shdmax = gld(sf + NMP_F_SHDMAX * ld);
-  const int32_t* si = a.static_i + c0;
-  c.lutyp = gld(si + NMP_I_VEGTYP * ld); c.sltyp = gld(si + NMP_I_SOILTYP * ld);
-  c.isc = gld(si + NMP_I_SOILCOLOR * ld);
-  c.ist = gld(si + NMP_I_IST * ld); c.ice = gld(si + NMP_I_ICE * ld);
-  const T* fc = a.forcing + c0;
-  c.sfctmp = gld(fc + NMP_A_SFCTMP * ld); c.sfcprs = gld(fc + NMP_A_SFCPRS * ld); c.psfc = gld(fc + NMP_A_PSFC * ld);
-  c.uu = gld(fc + NMP_A_UU * ld); c.vv = gld(fc + NMP_A_VV * ld); c.q2 = gld(fc + NMP_A_Q2 * ld);
-  c.soldn = gld(fc + NMP_A_SOLDN * ld); c.lwdn = gld(fc + NMP_A_LWDN * ld);
-  c.cosz = gld(fc + NMP_A_COSZ * ld);
-  c.status = 0;
 
   const Sink<T> out{a.diag ? a.diag + c0 : nullptr, a.state + c0, ld, a.diag_level, sf, si, fc,
                     a.isnow + c0, a.cost ? a.cost + c0 : nullptr,
@@ -2992,6 +3060,22 @@ extern "C" int nmp_debug_phase_cycles(unsigned long long* out16, int reset) {
   return r ? r : phase_cycles_tu8(out16, reset);
 }
 #endif
+#endif
+
+#if defined(NMP_DEBUG_DUMP) && (!defined(NMP_TU) || NMP_TU == 8)
+// debug dump (tools/mcse_probe.py): col >= 0 selects the column the next launches
+// dump (and clears the buffer to NaN); out (256 doubles) receives the buffer
+extern "C" int nmp_debug_dump(long long col, double* out) {
+  if (col >= 0) {
+    double nan[256];
+    for (int i = 0; i < 256; ++i) nan[i] = __builtin_nan("");
+    if (hipMemcpyToSymbol(HIP_SYMBOL(nmp_dbg), nan, sizeof(nan)) != hipSuccess) return -4;
+    if (hipMemcpyToSymbol(HIP_SYMBOL(nmp_dbg_col), &col, sizeof(col)) != hipSuccess) return -4;
+  }
+  if (out && hipMemcpyFromSymbol(out, HIP_SYMBOL(nmp_dbg), 256 * sizeof(double)) != hipSuccess)
+    return -4;
+  return 0;
+}
 #endif
 
 #if defined(NMP_WAVE_TIMING) && (!defined(NMP_TU) || NMP_TU == 4)

@@ -130,10 +130,36 @@ __device__ __forceinline__ T p5(T x) { return x * p4(x); }
 // operands (and overflow) their IEEE results and the quotient its sign.  (A
 // branch back to IEEE `/` for non-finite results instead measured slower than
 // plain `/`: profiles/r02/fp64_div.txt.)
+// Valid range: the 1-ulp bound needs 1/b normal and the quotient and the
+// residual b*q - a clear of underflow, i.e. 2^-1021 < |b| < 2^1021 and a
+// normal quotient.  For |b| >= 2^1022 the reciprocal is subnormal or flushes
+// and for subnormal b it overflows, so the result is NOT the IEEE quotient
+// there (tests/test_gpu_routines.py pins both sides).  Every divisor these
+// loops see is a physical resistance, conductance, temperature or height,
+// many decades inside the range.
 template <class T>
 __device__ __forceinline__ T dv(T a, T b) {
   return a / b;
 }
+#if defined(NMP_F32_DIV)
+// timing probes of shorter fp32 division sequences (tools only, NOT shipped):
+// 9 = v_rcp + one Newton step + two residual corrections + div_fixup (the IEEE
+// sequence without div_scale / div_fmas), 7 = one residual correction
+template <>
+__device__ __forceinline__ float dv<float>(float a, float b) {
+  float r = __builtin_amdgcn_rcpf(b);
+  float e = __builtin_fmaf(-b, r, 1.0f);
+  r = __builtin_fmaf(e, r, r);
+  float q = a * r;
+  e = __builtin_fmaf(-b, q, a);
+  q = __builtin_fmaf(e, r, q);
+#if NMP_F32_DIV == 9
+  e = __builtin_fmaf(-b, q, a);
+  q = __builtin_fmaf(e, r, q);
+#endif
+  return __builtin_amdgcn_div_fixupf(q, b, a);
+}
+#endif
 template <>
 __device__ __forceinline__ double dv<double>(double a, double b) {
 #ifdef NMP_F64_IEEE_DIV

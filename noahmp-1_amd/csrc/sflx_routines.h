@@ -167,6 +167,23 @@ DEV T frh2o(T smcmax, T psisat, T bexp, T tkelv, T smc, T sh2o, int& status) {
   return free_;
 }
 
+// calhum: func.f90:3958-3984 -- saturation mixing ratio (returned in g/g) and
+// its temperature derivative.  The constant sub-expressions (ELWV/RV, 1./A3,
+// A2*(A3-A4)) are folded by the reference's compiler in default real, which
+// rounds exactly as these run-time operations do.
+template <class T, bool R>
+DEV void calhum(T sfctmp, T sfcprs, T& q2sat, T& dqsdt2) {
+  typedef Mth<T, R> M;
+  const T A2 = L(17.67), A3 = L(273.15), A4 = L(29.65), ELWV = L(2.501E6);
+  const T A23M4 = A2 * (A3 - A4), E0 = L(0.611), RV = L(461.0), EPS = L(0.622);
+  const T es = E0 * M::exp(ELWV / RV * (L(1.) / A3 - L(1.) / sfctmp));
+  const T sfcprsx = sfcprs * L(1.E-3);
+  q2sat = EPS * es / (sfcprsx - es);
+  q2sat = q2sat * L(1.E3);
+  dqsdt2 = (q2sat / (L(1.0) + q2sat)) * A23M4 / p2(sfctmp - A4);
+  q2sat = q2sat / L(1.E3);
+}
+
 // rosr12 Thomas solve on layers kt..NL-1 (func.f90:4240-4288), static slots
 template <class T, int NL>
 DEV void rosr12(T (&p)[NL], const T (&a)[NL], const T (&b)[NL], T (&c)[NL], const T (&d)[NL],

@@ -156,8 +156,14 @@ class OfflineDriver:
         self.cs = ColumnState.from_host(cols, self.dev, self.dtype)
         # column ranges on their own streams: launch tails overlap (engine.StreamShards)
         self.ranges = StreamShards(self.engine, self.cs, streams)
+        total, first = self.cs.ncol, 0
+        if dist.is_initialized():
+            total = _global_count(self.cs.ncol, self.dev)
+            first = shard.shard_range(total, dist.get_rank(), dist.get_world_size())[0]
         if forcing == "device":
-            forcing = DeviceSyntheticForcing(cases.climate(cols), seed=0)
+            # draws keyed by the global column index: the forcing of a column
+            # does not depend on the world size
+            forcing = DeviceSyntheticForcing(cases.climate(cols), seed=0, first_col=first)
         self.forcing = forcing or SyntheticForcing(cols)
         self.dev_forcing = None
         if getattr(self.forcing, "on_device", False):
@@ -175,7 +181,6 @@ class OfflineDriver:
         self.upload = ForcingUpload(self.cs.ncol, self.dtype, self.dev)
         self.gather = None
         if dist.is_initialized():
-            total = _global_count(self.cs.ncol, self.dev)
             self.gather = shard.DiagGather(L.NDIAG_OUT, total, self.dtype, self.dev, dst=0)
             if self.gather.n_local != self.cs.ncol:
                 raise ValueError(f"rank {dist.get_rank()} holds {self.cs.ncol} columns, its "
@@ -266,7 +271,11 @@ class OfflineDriver:
             t0 = self.t
             t1 = t0 + cfg.timestep
             out = _is_boundary(t1, cfg.begdatetime, out_every) and self.write
-            pre, after = None, self.upload.stream
+            # the ranges wait for the caller's current stream (state set-up,
+            # restart copies, the gather fence assemble() left there) and, for
+            # host forcing, for the upload of this step's buffer
+            cur = torch.cuda.current_stream(self.dev)
+            pre, after = None, (cur, self.upload.stream)
             if self.dev_forcing is not None:
                 clim, fbuf = self.dev_forcing
                 f = fbuf[self.step_index % 2]
@@ -274,7 +283,7 @@ class OfflineDriver:
                 pre = lambda st, rng: self.engine.forcing_synth(  # noqa: E731
                     clim, jul, yl, self.forcing.seed, k, f, self.forcing.first_col, stream=st,
                     cols=rng)
-                after = torch.cuda.current_stream(self.dev)
+                after = cur
             else:
                 f = self.upload.put(self.forcing(self.step_index, t0))
             diag = self.diag

@@ -197,6 +197,58 @@ class Engine:
                                                int(step), int(first_col) + lo, _ptr(out, lo),
                                                C.c_void_p(s.cuda_stream)), "nmp_forcing_synth")
 
+    # ---- the reference's other public routines (nmp_frh2o / nmp_calhum) ------
+    def frh2o(self, sltyp, tkelv, smc, sh2o, status=None, stream=None):
+        """frh2o (func.f90:4494-4598) elementwise.  Device tensors (engine
+        precision, int32 sltyp) -> a new tensor of FREE, enqueued on `stream`;
+        numpy arrays -> numpy (nmp_frh2o_host, synchronous).  `status` (int32,
+        same kind as the inputs) receives NMP_ST_FLERCH / NMP_ST_STOP bits."""
+        n = int(len(tkelv))
+        if isinstance(tkelv, np.ndarray):
+            rt = np.float32 if self.precision == 4 else np.float64
+            a = [np.ascontiguousarray(x, rt) for x in (tkelv, smc, sh2o)]
+            si = np.ascontiguousarray(sltyp, np.int32)
+            out = np.empty(n, rt)
+            st = status if status is not None else np.zeros(n, np.int32)
+            assert st.dtype == np.int32 and st.flags.c_contiguous and st.shape == (n,)
+            _lib.check(self._lib.nmp_frh2o_host(self._h, n, C.c_void_p(si.ctypes.data),
+                                                *[C.c_void_p(x.ctypes.data) for x in a],
+                                                C.c_void_p(out.ctypes.data),
+                                                C.c_void_p(st.ctypes.data)), "nmp_frh2o_host")
+            return out
+        for t in (tkelv, smc, sh2o):
+            assert t.dtype == self.dtype and t.is_contiguous() and t.shape == (n,)
+            assert t.device.type == "cuda" and t.device.index == self.device
+        assert sltyp.dtype == torch.int32 and sltyp.is_contiguous() and sltyp.shape == (n,)
+        out = torch.empty(n, dtype=self.dtype, device=tkelv.device)
+        s = stream if stream is not None else torch.cuda.current_stream(self.device)
+        _lib.check(self._lib.nmp_frh2o(self._h, n, _ptr(sltyp), _ptr(tkelv), _ptr(smc), _ptr(sh2o),
+                                       _ptr(out), _ptr(status), C.c_void_p(s.cuda_stream)),
+                   "nmp_frh2o")
+        return out
+
+    def calhum(self, sfctmp, sfcprs, stream=None):
+        """calhum (func.f90:3958-3984) elementwise -> (Q2SAT, DQSDT2); device
+        tensors (enqueued on `stream`) or numpy arrays (synchronous)."""
+        n = int(len(sfctmp))
+        if isinstance(sfctmp, np.ndarray):
+            rt = np.float32 if self.precision == 4 else np.float64
+            t, p = (np.ascontiguousarray(x, rt) for x in (sfctmp, sfcprs))
+            q, d = np.empty(n, rt), np.empty(n, rt)
+            _lib.check(self._lib.nmp_calhum_host(self._h, n, C.c_void_p(t.ctypes.data),
+                                                 C.c_void_p(p.ctypes.data), C.c_void_p(q.ctypes.data),
+                                                 C.c_void_p(d.ctypes.data)), "nmp_calhum_host")
+            return q, d
+        for x in (sfctmp, sfcprs):
+            assert x.dtype == self.dtype and x.is_contiguous() and x.shape == (n,)
+            assert x.device.type == "cuda" and x.device.index == self.device
+        q = torch.empty(n, dtype=self.dtype, device=sfctmp.device)
+        d = torch.empty_like(q)
+        s = stream if stream is not None else torch.cuda.current_stream(self.device)
+        _lib.check(self._lib.nmp_calhum(self._h, n, _ptr(sfctmp), _ptr(sfcprs), _ptr(q), _ptr(d),
+                                        C.c_void_p(s.cuda_stream)), "nmp_calhum")
+        return q, d
+
     def sflx_columns(self, rec: np.ndarray) -> np.ndarray:
         """noahmp_sflx with the reference calling sequence on host records
         (layout.sflx_args_dtype(); nmp_sflx_columns), updated in place and returned.
@@ -276,20 +328,24 @@ class StreamShards:
 
     def step(self, forcing: torch.Tensor, zsoil, dt: float, julian: float, yearlen: int,
              diag: torch.Tensor | None = None, diag_level: int = L.DIAG_NONE, events=None,
-             after: torch.cuda.Stream | None | str = "current", pre=None):
-        """One step of every range.  `after`: the stream whose pending work (the
-        forcing upload, a previous reader of `diag`) each range waits for first
-        -- by default the caller's current stream, where torch enqueues uploads;
-        tensors are kept alive until the ranges are done with them.  Pass None
-        only when the inputs are known to be complete (e.g. after a synchronize).
+             after="current", pre=None):
+        """One step of every range.  `after`: the stream, or a tuple of streams,
+        whose pending work (the forcing upload, a previous reader of `diag`)
+        each range waits for first -- by default the caller's current stream,
+        where torch enqueues uploads; tensors are kept alive until the ranges
+        are done with them.  Pass None only when the inputs are known to be
+        complete (e.g. after a synchronize).
         events: per-range (start, end) pairs.  pre(stream, (lo, hi)): work
         enqueued on each range's stream before its step (e.g. generating that
         range's forcing on the device, Engine.forcing_synth)."""
-        if after == "current":
+        if isinstance(after, str) and after == "current":
             after = torch.cuda.current_stream(self.streams[0].device)
+        if after is not None and not isinstance(after, (tuple, list)):
+            after = (after,)
         for i, (st, rng) in enumerate(zip(self.streams, self.ranges)):
             if after is not None:
-                st.wait_stream(after)
+                for a in after:
+                    st.wait_stream(a)
                 forcing.record_stream(st)
                 if diag is not None:
                     diag.record_stream(st)

@@ -95,7 +95,8 @@ class DiagGather:
         self.host = [torch.zeros(nslot * self.slot, dtype=dtype) for _ in range(nbuf)] \
             if self.staged else None
         self.comm = comm
-        self.pending = [None] * nbuf
+        self.pending = [None] * nbuf   # host-side work handles (CPU buffers)
+        self.done = [None] * nbuf      # CUDA buffers: event after buffer b's last collective
         self.local_producers = [[] for _ in range(nbuf)]
 
     def _slot(self, buf: torch.Tensor, r: int) -> torch.Tensor:
@@ -128,11 +129,27 @@ class DiagGather:
                 self.comm.wait_stream(s)
             with torch.cuda.stream(self.comm):
                 self._issue(b, bufs[b], async_op=True)
+                self._fence(b)
         else:
             if self.device.type == "cuda":
                 for s in producers:
                     torch.cuda.current_stream(self.device).wait_stream(s)
             self._issue(b, bufs[b], async_op=True)
+            self._fence(b)
+
+    def _fence(self, b: int):
+        """CUDA buffers: the issuing stream waits for buffer b's collective (a
+        device-side wait, the host does not block) and an event recorded after
+        it becomes the buffer's fence.  It stays in place until the buffer's
+        next collective, so every later writer (`release`, however many
+        times) and reader (`assemble`) is ordered after the transfer -- none
+        can consume the fence and leave another stream unordered."""
+        if self.device.type != "cuda" or self.pending[b] is None:
+            return
+        self.pending[b].wait()
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(self.device))
+        self.done[b], self.pending[b] = ev, None
 
     def _issue(self, b: int, buf: torch.Tensor, async_op: bool):
         own = self._slot(buf, self.rank if self.receives else 0)
@@ -151,15 +168,14 @@ class DiagGather:
     def release(self, b: int, streams=()):
         """Make `streams` (default: the current stream) wait until the collective
         that last used buffer b is done, so it can be written again."""
+        if self.done[b] is not None:
+            for s in (streams or [torch.cuda.current_stream(self.device)]):
+                s.wait_event(self.done[b])
+            return
         w = self.pending[b]
         if w is None:
             return
-        if streams and self.device.type == "cuda":
-            for s in streams:
-                with torch.cuda.stream(s):
-                    w.wait()
-        else:
-            w.wait()
+        w.wait()  # CPU buffers: blocks the host until the collective is done
         self.pending[b] = None
 
     def assemble(self, b: int) -> torch.Tensor | None:

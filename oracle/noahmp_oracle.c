@@ -2785,6 +2785,11 @@ void oracle_tdfcnd(const nmp_params* P, int32_t n, const int32_t* sltyp, const r
   for (int32_t i = 0; i < n; ++i) out[i] = tdfcnd(P, sltyp[i], smc[i], sh2o[i]);
 }
 
+void oracle_calhum(int32_t n, const real* sfctmp, const real* sfcprs, real* q2sat,
+                   real* dqsdt2) {
+  for (int32_t i = 0; i < n; ++i) calhum(sfctmp[i], sfcprs[i], &q2sat[i], &dqsdt2[i]);
+}
+
 void oracle_frh2o(const nmp_params* P, int32_t n, const int32_t* sltyp, const real* tk,
                   const real* smc, const real* sh2o, real* out, int32_t* status) {
   for (int32_t i = 0; i < n; ++i) {

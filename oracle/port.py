@@ -136,8 +136,8 @@ def run(P: dict, options, zsoil, dt, yearlen, julian0, state, isnow, static_f, s
 
 
 # ---- single routines (the code sflx_column calls), fp32 bit-exact build ----
-def _rt(name, *argtypes):
-    lib, _ = _lib(4)
+def _rt(name, *argtypes, precision: int = 4):
+    lib, _ = _lib(precision)
     f = getattr(lib, name)
     f.argtypes = list(argtypes)
     f.restype = None
@@ -163,16 +163,28 @@ def tdfcnd(P: dict, sltyp, smc, sh2o):
     return out
 
 
-def frh2o(P: dict, sltyp, tk, smc, sh2o):
-    f32p = np.ctypeslib.ndpointer(np.float32, flags="C_CONTIGUOUS")
+def frh2o(P: dict, sltyp, tk, smc, sh2o, precision: int = 4):
+    rt = np.float32 if precision == 4 else np.float64
+    rp = np.ctypeslib.ndpointer(rt, flags="C_CONTIGUOUS")
     i32p = np.ctypeslib.ndpointer(np.int32, flags="C_CONTIGUOUS")
     n = len(tk)
-    out = np.zeros(n, np.float32)
+    out = np.zeros(n, rt)
     st = np.zeros(n, np.int32)
-    _rt("oracle_frh2o", C.c_char_p, C.c_int32, i32p, f32p, f32p, f32p, f32p, i32p)(
-        pack_params(P), n, np.ascontiguousarray(sltyp, np.int32), np.ascontiguousarray(tk, np.float32),
-        np.ascontiguousarray(smc, np.float32), np.ascontiguousarray(sh2o, np.float32), out, st)
+    _rt("oracle_frh2o", C.c_char_p, C.c_int32, i32p, rp, rp, rp, rp, i32p, precision=precision)(
+        pack_params(P), n, np.ascontiguousarray(sltyp, np.int32), np.ascontiguousarray(tk, rt),
+        np.ascontiguousarray(smc, rt), np.ascontiguousarray(sh2o, rt), out, st)
     return out, st
+
+
+def calhum(sfctmp, sfcprs, precision: int = 4):
+    """calhum (func.f90:3958-3984) over arrays: (Q2SAT, DQSDT2)."""
+    rt = np.float32 if precision == 4 else np.float64
+    rp = np.ctypeslib.ndpointer(rt, flags="C_CONTIGUOUS")
+    n = len(sfctmp)
+    q, d = np.zeros(n, rt), np.zeros(n, rt)
+    _rt("oracle_calhum", C.c_int32, rp, rp, rp, rp, precision=precision)(
+        n, np.ascontiguousarray(sfctmp, rt), np.ascontiguousarray(sfcprs, rt), q, d)
+    return q, d
 
 
 def rosr12(kt, a, b, c, d):

@@ -77,6 +77,8 @@ def _load():
                                        f32p, i32p, f32p, i32p, f32p, f32p, i32p]
         if hasattr(lib, "ref_frh2o"):
             lib.ref_frh2o.argtypes = [C.c_int32, i32p, f32p, f32p, f32p, f32p, i32p]
+        if hasattr(lib, "ref_calhum"):
+            lib.ref_calhum.argtypes = [C.c_int32, f32p, f32p, f32p, f32p]
         if hasattr(lib, "ref_set_ficeold"):
             lib.ref_set_ficeold.argtypes = [C.c_void_p, C.c_int32]
         if hasattr(lib, "ref_sflx_run"):
@@ -189,3 +191,15 @@ def frh2o(sltyp, tk, smc, sh2o):
                       np.ascontiguousarray(smc, np.float32), np.ascontiguousarray(sh2o, np.float32),
                       out, st)
     return out, st
+
+
+def calhum(sfctmp, sfcprs):
+    """The reference's calhum (func.f90:3958-3984) over arrays: (Q2SAT, DQSDT2)."""
+    lib = _load()
+    n = len(sfctmp)
+    q = np.zeros(n, np.float32)
+    d = np.zeros(n, np.float32)
+    with _lock:
+        lib.ref_calhum(n, np.ascontiguousarray(sfctmp, np.float32),
+                       np.ascontiguousarray(sfcprs, np.float32), q, d)
+    return q, d

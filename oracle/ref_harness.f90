@@ -60,7 +60,7 @@ end subroutine wrf_error_fatal
 module ref_harness
   use iso_c_binding
   use noahmp_global
-  use noahmp_func, only: noahmp_sflx, frh2o
+  use noahmp_func, only: noahmp_sflx, frh2o, calhum
   use ref_status
   implicit none
   integer, parameter :: NST = 56, NSF = 6, NSI = 6, NFC = 12, NDG = 58
@@ -235,6 +235,18 @@ contains
        stat(i) = cur_status
     end do
   end subroutine ref_frh2o
+
+  ! calhum (func.f90:3958-3984): a module procedure of noahmp_func, public by
+  ! default (the module's private list does not name it), called directly.
+  subroutine ref_calhum(n, sfctmp, sfcprs, q2sat, dqsdt2) bind(C, name='ref_calhum')
+    integer(c_int32_t), value :: n
+    real(c_float), intent(in) :: sfctmp(n), sfcprs(n)
+    real(c_float), intent(out) :: q2sat(n), dqsdt2(n)
+    integer :: i
+    do i = 1, n
+       call calhum(sfctmp(i), sfcprs(i), q2sat(i), dqsdt2(i))
+    end do
+  end subroutine ref_calhum
 
   subroutine one_column(c, dt, yearlen, julian, zsoil_in, s, isn, sf, si, fc, d, stat)
     integer, intent(in) :: c, yearlen

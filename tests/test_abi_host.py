@@ -82,7 +82,7 @@ def test_params_struct_size():
 
 
 def test_abi_version_and_errors(engine_lib):
-    assert engine_lib.nmp_abi_version() == 3
+    assert engine_lib.nmp_abi_version() == 4
     for code in (0, -1, -2, -3, -4, -5, -99):
         assert engine_lib.nmp_strerror(code)
     p = _lib.NmpParams()

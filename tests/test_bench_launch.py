@@ -1,0 +1,77 @@
+"""bench.py's N-rank launch (VERDICT r2 "missing 2"): `bench.py --gpus N`
+without a launcher starts N ranks itself, and any failure -- a rank dying, a
+WORLD_SIZE that disagrees with --gpus, too few GPUs for RCCL -- is a non-zero
+exit with no result line, never a one-GPU line under an N-GPU label.
+
+CPU tests run the launcher with --launch-probe (ranks rendezvous over gloo and
+report, no GPU); the GPU test runs real N = 2 steps with both ranks on the
+box's one device (NMP_BENCH_BACKEND=gloo, the rehearsal backend)."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BENCH = os.path.join(ROOT, "bench.py")
+
+
+def run(args, timeout=180, **env):
+    e = dict(os.environ, **env)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        if k not in env:
+            e.pop(k, None)
+    p = subprocess.run([sys.executable, BENCH, *args], capture_output=True, text=True,
+                       timeout=timeout, env=e)
+    lines = [json.loads(x) for x in p.stdout.splitlines() if x.startswith("{")]
+    return p.returncode, lines, p.stderr
+
+
+@pytest.mark.parametrize("n", [2, 3])
+def test_spawned_ranks_report_world(n):
+    rc, lines, err = run(["--gpus", str(n), "--launch-probe", "--ncol", "500"])
+    assert rc == 0, err[-2000:]
+    assert len(lines) == 1, lines
+    ln = lines[0]
+    assert ln["n_gpus"] == n and ln["ranks_joined"] == n
+    assert ln["ncol_total"] == n * 500 and ln["first_col_sum"] == 500 * n * (n - 1) // 2
+
+
+def test_failed_rank_fails_the_job():
+    rc, lines, err = run(["--gpus", "2", "--launch-probe", "--ncol", "500"],
+                         NMP_BENCH_FAIL_RANK="1")
+    assert rc != 0 and not lines
+    assert "rank 1 exited" in err
+
+
+def test_world_size_must_match_gpus():
+    rc, lines, err = run(["--gpus", "4", "--launch-probe", "--ncol", "500"], WORLD_SIZE="1",
+                         RANK="0", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT="29555")
+    assert rc != 0 and not lines and "WORLD_SIZE 1" in err
+
+
+def test_rccl_needs_one_gpu_per_rank():
+    """With the default backend (RCCL) the launcher counts devices first: this
+    container has none, so --gpus 2 must fail before starting any rank."""
+    import torch
+    if torch.cuda.device_count() >= 2:
+        pytest.skip("enough GPUs here")
+    rc, lines, err = run(["--gpus", "2", "--ncol", "500", "--no-cpu-baseline"])
+    assert rc == 2 and not lines and "visible GPUs" in err
+
+
+@pytest.mark.gpu
+def test_bench_two_ranks_on_the_gpu():
+    """A real N = 2 bench line from `bench.py --gpus 2` alone: both ranks step
+    their shard through the HIP engine (sharing the box's one GPU; gloo for the
+    gather), output every step gathered to rank 0."""
+    rc, lines, err = run(["--gpus", "2", "--ncol", "8192", "--steps", "4", "--warmup", "1",
+                          "--out-every", "2", "--no-cpu-baseline", "--period", "4"],
+                         timeout=240, NMP_BENCH_BACKEND="gloo")
+    assert rc == 0, err[-3000:]
+    assert len(lines) == 1, lines
+    ln = lines[0]
+    assert ln["n_gpus"] == 2 and ln["config"]["ncol_total"] == 2 * 8192
+    assert ln["value"] > 0 and ln["checks"]["stc_finite"]
+    assert ln["config"]["backend"] == "gloo"

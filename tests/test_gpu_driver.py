@@ -240,3 +240,48 @@ def test_driver_device_forcing_equals_engine_steps(engine_lib, tmp_path):
 def timeman_julian(cfg):
     from noahmp_amd import timeman
     return timeman.julian(cfg.begdatetime)
+
+
+def _device_forcing_rank(rank, world, port, nml, out_dir, n):
+    """One rank of a device-forcing run: its shard_range block of the n columns."""
+    import torch.distributed as dist
+    from noahmp_amd import shard
+    from noahmp_amd.params import Params
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    cfg = config.Config(nml)
+    cols = cases.make_columns(n, "mixed", Params.builtin().as_dict(), seed=12,
+                              julian=timeman_julian(cfg))
+    s0, cnt = shard.shard_range(n, rank, world)
+    drv = driver.OfflineDriver(cfg, cols.take(np.arange(s0, s0 + cnt)), forcing="device",
+                               write=False).run(nsteps=6)
+    np.savez(os.path.join(out_dir, f"dev{rank}.npz"), state=drv.cs.state.cpu().numpy())
+    dist.barrier()
+    drv.engine.close()
+    dist.destroy_process_group()
+
+
+def test_driver_device_forcing_independent_of_world_size(engine_lib, tmp_path):
+    """forcing="device" under a process group keys every draw by the global
+    column index (first_col = the rank's shard_range start): two ranks give
+    each column the forcing, hence the state, of the one-rank run, bit for bit
+    (every rank used to draw rank 0's numbers)."""
+    import socket
+    import torch.multiprocessing as mp
+    from noahmp_amd.params import Params
+    from test_config import write_case
+    n = 20_001
+    nml = write_case(tmp_path)
+    cfg = config.Config(nml)
+    cols = cases.make_columns(n, "mixed", Params.builtin().as_dict(), seed=12,
+                              julian=timeman_julian(cfg))
+    one = driver.OfflineDriver(cfg, cols, forcing="device", write=False).run(nsteps=6)
+    ref = one.cs.state.cpu().numpy()
+    one.engine.close()
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    mp.start_processes(_device_forcing_rank, args=(2, port, str(nml), str(tmp_path), n),
+                       nprocs=2, start_method="spawn")
+    got = np.concatenate([np.load(tmp_path / f"dev{r}.npz")["state"] for r in range(2)], axis=1)
+    assert bit_equal(got, ref).all()

@@ -179,3 +179,125 @@ def test_device_fp64_loop_division(rt):
     assert np.array_equal(q[sp], host[sp], equal_nan=True)
     num = sp & ~np.isnan(host)  # (a NaN's sign bit is not specified)
     assert np.array_equal(np.signbit(q[num]), np.signbit(host[num]))
+
+
+def calhum_inputs(n, seed):
+    """Canopy temperatures 220-330 K, surface pressures 50-110 kPa."""
+    rng = np.random.default_rng(seed)
+    return (rng.uniform(220.0, 330.0, n).astype(np.float32),
+            rng.uniform(5.0e4, 1.1e5, n).astype(np.float32))
+
+
+def test_calhum_restatement_vs_reference(oracle_port):
+    """calhum (func.f90:3958-3984, public by default) of the C restatement ==
+    the reference's own (oracle/_ref ref_calhum), bit for bit."""
+    import ref
+    if not ref.available():
+        pytest.skip("reference oracle not built (oracle/_ref)")
+    t, p = calhum_inputs(50000, 6)
+    q, d = ref.calhum(t, p)
+    q2, d2 = oracle_port.calhum(t, p)
+    assert bit_equal(q2, q).all() and bit_equal(d2, d).all()
+
+
+@pytest.fixture(scope="module")
+def engines():
+    from noahmp_amd import layout as L
+    from noahmp_amd.engine import Engine
+    from noahmp_amd.params import Params
+    P = Params.builtin("STAS", "USGS")
+    e = {prec: Engine(P, dict(L.CASE_NML_OPTIONS), device=0, precision=prec) for prec in (4, 8)}
+    yield e
+    for x in e.values():
+        x.close()
+
+
+@pytest.mark.gpu
+def test_abi_frh2o_vs_reference(engines, oracle_port):
+    """nmp_frh2o / nmp_frh2o_host (the product library's export of the
+    reference's public frh2o, func.f90:4494-4598): fp32 bit for bit with the
+    reference (and its Flerchinger status), device and host entries equal;
+    fp64 within 1e-5 of it; a soil type outside the tables gives NaN + STOP."""
+    import torch
+    import ref
+    P, slt, tk, smc, sh2o = frh2o_inputs(50000, 7)
+    e4 = engines[4]
+    st = np.zeros(tk.size, np.int32)
+    got = e4.frh2o(slt, tk, smc, sh2o, status=st)
+    want, wst = oracle_port.frh2o(P, slt, tk, smc, sh2o)
+    assert bit_equal(got, want).all(), int((~bit_equal(got, want)).sum())
+    assert np.array_equal(st, wst)
+    if ref.available():
+        ref.configure(tuple(int(x) for x in (1,) * 12))
+        rv, rs = ref.frh2o(slt, tk, smc, sh2o)
+        assert bit_equal(got, rv).all()
+        assert np.array_equal(st != 0, rs != 0)
+    dev = "cuda:0"
+    T = [torch.as_tensor(x, device=dev) for x in (slt, tk, smc, sh2o)]
+    dst = torch.zeros(tk.size, dtype=torch.int32, device=dev)
+    out = e4.frh2o(*T, status=dst)
+    torch.cuda.synchronize()
+    assert bit_equal(out.cpu().numpy(), got).all() and np.array_equal(dst.cpu().numpy(), st)
+    # fp64: against the fp64 restatement (1e-9, ocml vs glibc double libm);
+    # against the fp32 reference only within the Newton loop's own 0.005
+    # convergence step, which one more or fewer iteration moves the result by
+    g8 = engines[8].frh2o(slt, tk, smc, sh2o)
+    w8, _ = oracle_port.frh2o(P, slt, tk, smc, sh2o, precision=8)
+    assert g8.dtype == np.float64
+    assert (np.abs(g8 - w8) <= 1e-9 * (1 + np.abs(w8))).mean() >= 0.99
+    assert np.abs(g8 - want).max() <= 0.01
+    bad = np.zeros(2, np.int32)
+    v = e4.frh2o(np.array([0, 31], np.int32), tk[:2], smc[:2], sh2o[:2], status=bad)
+    assert np.isnan(v).all() and (bad == 128).all()
+
+
+@pytest.mark.gpu
+def test_abi_calhum_vs_reference(engines, oracle_port):
+    """nmp_calhum / nmp_calhum_host (calhum, func.f90:3958-3984): fp32 bit for
+    bit with the reference's own calhum, device == host entry, fp64 within
+    1e-6 relative."""
+    import torch
+    import ref
+    t, p = calhum_inputs(50000, 8)
+    q, d = engines[4].calhum(t, p)
+    wq, wd = oracle_port.calhum(t, p)
+    assert bit_equal(q, wq).all() and bit_equal(d, wd).all()
+    if ref.available():
+        rq, rd = ref.calhum(t, p)
+        assert bit_equal(q, rq).all() and bit_equal(d, rd).all()
+    tq, td = engines[4].calhum(torch.as_tensor(t, device="cuda:0"),
+                               torch.as_tensor(p, device="cuda:0"))
+    torch.cuda.synchronize()
+    assert bit_equal(tq.cpu().numpy(), q).all() and bit_equal(td.cpu().numpy(), d).all()
+    q8, d8 = engines[8].calhum(t, p)
+    w8q, w8d = oracle_port.calhum(t, p, precision=8)
+    assert np.allclose(q8, w8q, rtol=1e-12) and np.allclose(d8, w8d, rtol=1e-12)
+    assert np.allclose(q8, wq, rtol=1e-5) and np.allclose(d8, wd, rtol=1e-5)
+
+
+@pytest.mark.gpu
+def test_device_fp64_loop_division_range(rt):
+    """The valid operand range stated at nmp::dv<double> (csrc/sflx_math.h):
+    divisors out to 2^+-1020 and quotients near both ends of the normal range
+    stay within 1 ulp of IEEE; the documented exceptions (|b| >= 2^1022,
+    subnormal b) are where the reciprocal leaves the normal range."""
+    rng = np.random.default_rng(10)
+    n = 20_000
+    e = rng.integers(-1020, 1021, n).astype(np.float64)
+    b = rng.choice([-1.0, 1.0], n) * rng.uniform(1.0, 2.0, n) * np.exp2(e)
+    ea = np.clip(e + rng.integers(-30, 31, n), -1020, 1020)  # |a/b| within 2^+-31
+    a = rng.uniform(1.0, 2.0, n) * np.exp2(ea)
+    a, b = np.ascontiguousarray(a), np.ascontiguousarray(b)
+    q, ieee = np.zeros_like(a), np.zeros_like(a)
+    assert rt.rt_dv64(n, a, b, q, ieee) == 0
+    ok = np.isfinite(ieee) & (np.abs(ieee) >= np.finfo(np.float64).tiny)
+    assert ok.mean() > 0.99
+    ulp = np.abs(q[ok] - ieee[ok]) / np.spacing(np.abs(ieee[ok]))
+    assert ulp.max() <= 1.0, ulp.max()
+    # outside the range: b = 2^1023 (reciprocal subnormal) is not exact
+    a2 = np.ascontiguousarray([1.5 * 2.0 ** 1000])
+    b2 = np.ascontiguousarray([1.75 * 2.0 ** 1023])
+    q2, i2 = np.zeros(1), np.zeros(1)
+    assert rt.rt_dv64(1, a2, b2, q2, i2) == 0
+    assert i2[0] == a2[0] / b2[0]
+    print("2^1023 divisor:", q2[0], "IEEE", i2[0])

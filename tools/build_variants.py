@@ -69,6 +69,9 @@ VARIANTS = {
     # timing probes only (NOT bit-exact): upper bounds of what faster division
     # / sqrt sequences could save
     "nocrdiv": ("-fno-hip-fp32-correctly-rounded-divide-sqrt",),
+    "fdiv9": {"f32": ["-DNMP_F32_DIV=9"]},
+    "ldswait0": {"f32": ["-DNMP_LDS_EXPLICIT_WAIT=0"]},
+    "fdiv7": {"f32": ["-DNMP_F32_DIV=7"]},
     "nopeel": ("-DNMP_VEGE_NOPEEL",),
     "vu2": ("-DNMP_VEGE_UNROLL=2",),
     "vu3": ("-DNMP_VEGE_UNROLL=3",),
@@ -87,6 +90,10 @@ VARIANTS = {
     "exhaust": ("-mllvm", "-exhaustive-register-search"),
     "defer": ("-mllvm", "-enable-deferred-spilling"),
     "nomcse": ("-mllvm", "-disable-machine-cse"),
+    # the fp64 translation unit alone without MachineCSE
+    "nomcse64": {"f64": ["-mllvm", "-disable-machine-cse"]},
+    "dbg64": {"f64": ["-DNMP_DEBUG_DUMP"]},
+    "nomcse64_dbg": {"f64": ["-mllvm", "-disable-machine-cse", "-DNMP_DEBUG_DUMP"]},
     "notaildup": ("-mllvm", "-disable-tail-duplicate", "-mllvm", "-disable-early-taildup"),
     "gvnsink": ("-mllvm", "-enable-gvn-sink"),
     "nolsv": ("-mllvm", "-amdgpu-load-store-vectorizer=false"),

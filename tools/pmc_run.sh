@@ -14,7 +14,12 @@ for C in FETCH_SIZE WRITE_SIZE; do
   rc=$?; echo "bench $C rc=$rc"; [ $rc -eq 0 ] || exit $rc
 done
 if [ "${VALU:-1}" = 1 ]; then
-  timeout -k 10 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVES SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR --kernel-trace --output-format csv -d "$OUT/bench_SQ" -o run -- python3 "$R/bench.py" --steps 5 --warmup 1 --no-cpu-baseline ${BENCH_ARGS:-} > "$OUT/bench_SQ.log" 2>&1
+  # two SQ passes (at most 8 SQ counters each): the VALU total, issue activity
+  # and memory instructions, then the VALU instruction classes the bench line's
+  # cycle-weighted VALU fraction needs (bench.py valu_weighted)
+  timeout -k 10 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVES SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_ACTIVE_INST_VALU SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_TRANS_F64 --kernel-trace --output-format csv -d "$OUT/bench_SQ" -o run -- python3 "$R/bench.py" --steps 5 --warmup 1 --no-cpu-baseline ${BENCH_ARGS:-} > "$OUT/bench_SQ.log" 2>&1
   rc=$?; echo "bench SQ rc=$rc"; [ $rc -eq 0 ] || exit $rc
+  timeout -k 10 300 rocprofv3 --pmc SQ_INSTS_VALU_ADD_F32 SQ_INSTS_VALU_MUL_F32 SQ_INSTS_VALU_FMA_F32 SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_FMA_F64 SQ_WAVES --kernel-trace --output-format csv -d "$OUT/bench_SQ2" -o run -- python3 "$R/bench.py" --steps 5 --warmup 1 --no-cpu-baseline ${BENCH_ARGS:-} > "$OUT/bench_SQ2.log" 2>&1
+  rc=$?; echo "bench SQ2 rc=$rc"; [ $rc -eq 0 ] || exit $rc
 fi
 find "$OUT" -name "*.csv" | head -20

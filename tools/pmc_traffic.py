@@ -83,12 +83,20 @@ def main():
            "write_correction": rw, "read_bytes": rd, "write_bytes": wr,
            "bytes_per_launch": rd + wr, "bytes_per_colstep": (rd + wr) / cols_per_launch,
            "source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes ({base})"}
-    sq = os.path.join(base, "bench_SQ")
-    if os.path.isdir(sq):
-        for c in ("SQ_INSTS_VALU", "SQ_WAVES", "SQ_INSTS_SALU", "SQ_INSTS_VMEM_RD",
-                  "SQ_INSTS_VMEM_WR"):
+    for sub, names in (("bench_SQ", ("SQ_INSTS_VALU", "SQ_WAVES", "SQ_INSTS_SALU",
+                                      "SQ_INSTS_VMEM_RD", "SQ_INSTS_VMEM_WR",
+                                      "SQ_ACTIVE_INST_VALU", "SQ_INSTS_VALU_INT32",
+                                      "SQ_INSTS_VALU_TRANS_F64")),
+                       ("bench_SQ2", ("SQ_INSTS_VALU_ADD_F32", "SQ_INSTS_VALU_MUL_F32",
+                                      "SQ_INSTS_VALU_FMA_F32", "SQ_INSTS_VALU_TRANS_F32",
+                                      "SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64",
+                                      "SQ_INSTS_VALU_FMA_F64"))):
+        sq = os.path.join(base, sub)
+        if not os.path.isdir(sq):
+            continue
+        for c in names:
             try:
-                res[c] = mean_for(sq, c, KERNEL)[0]
+                res[c] = mean_for(sq, c, KERNEL)[0]  # per dispatch
             except AssertionError:
                 pass
     out = os.path.join(ROOT, "profiles", "traffic.json")
