@@ -141,7 +141,21 @@ template <class T>
 __device__ __forceinline__ T dv(T a, T b) {
   return a / b;
 }
-#if defined(NMP_F32_DIV)
+#if defined(NMP_F32_DIV) && NMP_F32_DIV == 1
+// candidate: the IEEE lowering with ONE residual correction instead of two
+template <>
+__device__ __forceinline__ float dv<float>(float a, float b) {
+  bool num_scaled;
+  const float den = __builtin_amdgcn_div_scalef(a, b, false, &num_scaled);
+  const float num = __builtin_amdgcn_div_scalef(a, b, true, &num_scaled);
+  float r = __builtin_amdgcn_rcpf(den);
+  const float e0 = __builtin_fmaf(-den, r, 1.0f);
+  r = __builtin_fmaf(e0, r, r);
+  const float q = num * r;
+  const float e = __builtin_fmaf(-den, q, num);
+  return __builtin_amdgcn_div_fixupf(__builtin_amdgcn_div_fmasf(e, r, q, num_scaled), b, a);
+}
+#elif defined(NMP_F32_DIV)
 // timing probes of shorter fp32 division sequences (tools only, NOT shipped):
 // 9 = v_rcp + one Newton step + two residual corrections + div_fixup (the IEEE
 // sequence without div_scale / div_fmas), 7 = one residual correction

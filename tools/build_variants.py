@@ -70,6 +70,7 @@ VARIANTS = {
     # / sqrt sequences could save
     "nocrdiv": ("-fno-hip-fp32-correctly-rounded-divide-sqrt",),
     "fdiv9": {"f32": ["-DNMP_F32_DIV=9"]},
+    "cr9": {"f32": ["-DNMP_F32_DIV=1"]},
     "ldswait0": {"f32": ["-DNMP_LDS_EXPLICIT_WAIT=0"]},
     "fdiv7": {"f32": ["-DNMP_F32_DIV=7"]},
     "nopeel": ("-DNMP_VEGE_NOPEEL",),
@@ -123,8 +124,10 @@ if __name__ == "__main__":
             if "f32" in v:  # extra flags for the fp32 translation unit only
                 sf["sflx_kernel.hip"] = list(sf["sflx_kernel.hip"]) + list(v["f32"])
             return build.build(force=True, verbose=False, out=os.path.join(vdir, f"lib_{n}.so"),
-                               extra=tuple(v.get("extra", ())), source_flags=sf)
-        return build.build(force=True, verbose=False, out=os.path.join(vdir, f"lib_{n}.so"), extra=v)
+                               extra=tuple(v.get("extra", ())), source_flags=sf,
+                               check_asm=not n.startswith("nomcse"))
+        return build.build(force=True, verbose=False, out=os.path.join(vdir, f"lib_{n}.so"), extra=v,
+                           check_asm=not n.startswith("nomcse"))
     with ThreadPoolExecutor(2) as ex:
         list(ex.map(one, names))
     print("built", names)

@@ -54,6 +54,18 @@ __device__ __forceinline__ float div9(float a, float b) {
   q = __builtin_fmaf(e, r, q);
   return __builtin_amdgcn_div_fixupf(q, b, a);
 }
+// the IEEE lowering (div_scale / div_fmas keep every operand in range) with
+// ONE residual correction instead of two: 9 instructions instead of 11
+__device__ __forceinline__ float div_cr9(float a, float b) {
+  bool num_scaled;
+  const float den = __builtin_amdgcn_div_scalef(a, b, false, &num_scaled);
+  const float num = __builtin_amdgcn_div_scalef(a, b, true, &num_scaled);
+  const float r = rcp1(den);
+  const float q = num * r;
+  const float e = __builtin_fmaf(-den, q, num);
+  const float qs = __builtin_amdgcn_div_fmasf(e, r, q, num_scaled);
+  return __builtin_amdgcn_div_fixupf(qs, b, a);
+}
 __device__ __forceinline__ bool same(float x, float y) {
   return __float_as_uint(x) == __float_as_uint(y) || (x != x && y != y);
 }
@@ -77,6 +89,21 @@ __global__ void t1(unsigned long long* bad, unsigned* first) {
   if (nbad) atomicAdd(bad, nbad);
 }
 
+// T1b: rcp1 is exponent-independent: rcp1(m * 2^k) == rcp1(m) * 2^-k for every
+// significand m in [1, 2) and every k with m*2^k and its reciprocal normal
+__global__ void t1b(unsigned long long* bad) {
+  const unsigned mb = blockIdx.x * blockDim.x + threadIdx.x;
+  if (mb >= (1u << 23)) return;
+  const float m = __uint_as_float(0x3f800000u | mb);
+  const float r = rcp1(m);
+  unsigned long long n = 0;
+  for (int k = -125; k <= 125; ++k) {
+    const float rk = rcp1(ldexpf(m, k));
+    if (!same(rk, ldexpf(r, -k))) ++n;
+  }
+  if (n) atomicAdd(bad, n);
+}
+
 // T2: thread = one b significand, loops over a slice of a significands
 __global__ void t2(unsigned a0, unsigned na, unsigned long long* bad7,
                    unsigned long long* bad9, unsigned* ex7) {
@@ -93,6 +120,7 @@ __global__ void t2(unsigned a0, unsigned na, unsigned long long* bad7,
       ex7[1] = mb;
     }
     if (!same(div9(a, b), w)) ++n9;
+    if (!same(div_cr9(a, b), w)) ++n9;
   }
   if (n7) atomicAdd(bad7, n7);
   if (n9) atomicAdd(bad9, n9);
@@ -113,7 +141,7 @@ __device__ bool in_range(float a, float b) {
 }
 __global__ void t3(uint64_t seed, int n_per, unsigned long long* cnt) {
   const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  unsigned long long c[6] = {0, 0, 0, 0, 0, 0};  // [in,out] x {n, bad7, bad9}
+  unsigned long long c[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // [in,out] x {n, bad7, bad9}, cr9 bad
   for (int i = 0; i < n_per; ++i) {
     const uint64_t h = mix(seed ^ mix(tid * 7919 + i));
     float a = __uint_as_float((unsigned)h), b = __uint_as_float((unsigned)(h >> 32));
@@ -123,8 +151,9 @@ __global__ void t3(uint64_t seed, int n_per, unsigned long long* cnt) {
     ++c[k];
     if (!same(div7(a, b), w)) ++c[k + 1];
     if (!same(div9(a, b), w)) ++c[k + 2];
+    if (!same(div_cr9(a, b), w)) ++c[6 + k / 3];
   }
-  for (int k = 0; k < 6; ++k)
+  for (int k = 0; k < 8; ++k)
     if (c[k]) atomicAdd(&cnt[k], c[k]);
 }
 
@@ -149,6 +178,13 @@ int main(int argc, char** argv) {
   if (h[0]) std::printf(" (first 0x%08x)\n", hu[0]);
   std::fflush(stdout);
 
+  hipLaunchKernelGGL(t1b, dim3((1u << 23) / 256), dim3(256), 0, 0, d + 3);
+  CHECK(hipDeviceSynchronize());
+  CHECK(hipMemcpy(h, d, sizeof(h), hipMemcpyDeviceToHost));
+  std::printf("T1b rcp1(m 2^k) == rcp1(m) 2^-k for all m in [1,2), |k| <= 125: %llu mismatches\n",
+              h[3]);
+  std::fflush(stdout);
+
   // T2: a significands in t2_launches slices of 2^23/64
   const unsigned slice = (1u << 23) / 64;
   for (int L = 0; L < t2_launches && L < 64; ++L) {
@@ -157,8 +193,8 @@ int main(int argc, char** argv) {
     CHECK(hipDeviceSynchronize());
     if (L % 8 == 7 || L == t2_launches - 1) {
       CHECK(hipMemcpy(h, d, sizeof(h), hipMemcpyDeviceToHost));
-      std::printf("T2 %2d/64 slices: div7 mismatches %llu, div9 mismatches %llu\n", L + 1, h[1],
-                  h[2]);
+      std::printf("T2 %2d/64 slices: div7 mismatches %llu, div9 + cr9 mismatches %llu\n", L + 1,
+                  h[1], h[2]);
       std::fflush(stdout);
     }
   }
@@ -175,5 +211,7 @@ int main(int argc, char** argv) {
               "div7 bad %llu, div9 bad %llu\n", h[8], h[9], h[10]);
   std::printf("T3 random pairs outside that range (incl. inf/nan/subnormal): %llu, div7 bad %llu, "
               "div9 bad %llu\n", h[11], h[12], h[13]);
+  std::printf("T3 cr9 (div_scale + one correction + div_fmas) bad: inside %llu, outside %llu\n",
+              h[14], h[15]);
   return 0;
 }
