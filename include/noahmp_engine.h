@@ -263,7 +263,13 @@ int nmp_step(nmp_engine* eng, int64_t ncol, int64_t ld, const float zsoil[4], fl
  * only its own index in every array, so results are bit-identical for any
  * order.  nmp_rebin builds an order from such keys: within each tile of `tile`
  * consecutive columns (a multiple of 64), the columns sorted by key, so that
- * the waves of the next step hold columns of similar cost. */
+ * the waves of the next step hold columns of similar cost.
+ * PRECONDITION (not checked by the library): order must be a permutation of
+ * 0..ncol-1.  A duplicate entry makes two lanes step the same column at once
+ * (a data race on its state) and an entry outside [0, ncol) reads and writes
+ * outside the arrays; neither is reported.  Orders built by nmp_rebin satisfy
+ * it; the Python Engine.step checks a caller-supplied order when
+ * NMP_CHECK_ORDER=1. */
 int nmp_step_binned(nmp_engine* eng, int64_t ncol, int64_t ld, const float zsoil[4], float dt,
                     float julian, int32_t yearlen, void* state, int32_t* isnow,
                     const void* static_f, const int32_t* static_i, const void* forcing, void* diag,
@@ -385,6 +391,12 @@ int nmp_set_cols_per_wave(nmp_engine* eng, int cpw);
 int nmp_option_set(nmp_engine* eng, int request);
 
 int nmp_engine_info(const nmp_engine* eng, int* device, int* precision, nmp_options* opts);
+/* Diagnostic (no reference counterpart): how many column-steps of the fp32
+ * "ref" kernels re-ran the canopy Newton loop with the reference's IEEE
+ * divisions because an operand left the range where the loop's faster
+ * division is exact (DESIGN.md "Division in the canopy loop"); *out receives
+ * the count since the last reset, reset != 0 clears it.  Process-wide. */
+int nmp_div_redo_count(unsigned long long* out, int reset);
 void nmp_finalize(nmp_engine* eng);
 const char* nmp_strerror(int code);
 int nmp_abi_version(void);

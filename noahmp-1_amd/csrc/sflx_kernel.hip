@@ -220,10 +220,33 @@ struct Sfc1Logs {
   }
 };
 
-template <class T, bool R>
-DEV void sfcdif1(int iter, T sfctmp, T rhoair, T h, T qair, T zlvl, T zpd, const Sfc1Logs<T, R>& lg,
-                 T z0h, T ur, T mpe, T& moz, int& mozsgn, T& fm, T& fh, T& fm2, T& fh2, T& cm,
-                 T& ch, T& fv) {
+// The loop-invariant operands of sfcdif1's divisions (:3426-3432), formed
+// once per loop by the caller through the loop's division policy `d`:
+// KARMAN*(GRAV/TVIR), the reciprocal of RHOAIR*CPAIR, and the numerators
+// ZLVL-ZPD and 2+Z0H (d.chk).  Same values, bit for bit, as forming them in
+// every iteration as the reference does.
+template <class T>
+struct Sfc1Inv {
+  T kgtv;          // KARMAN * (GRAV / TVIR)
+  Recip<T> rhocp;  // RHOAIR * CPAIR
+  T dz, d2;        // ZLVL - ZPD, 2 + Z0H
+};
+template <class T, class D>
+DEV Sfc1Inv<T> sfc1_inv(D& d, T sfctmp, T qair, T rhoair, T zlvl, T zpd, T z0h) {
+  const T tvir = (L(1.0) + L(0.61) * qair) * sfctmp;
+  Sfc1Inv<T> v;
+  v.kgtv = KARMAN * d.divk(GRAV, d.rec(tvir));
+  v.rhocp = d.rec(rhoair * CPAIR);
+  v.dz = zlvl - zpd;
+  v.d2 = L(2.0) + z0h;
+  d.chk(v.dz);
+  d.chk(v.d2);
+  return v;
+}
+
+template <class T, bool R, class D>
+DEV void sfcdif1(D& d, const Sfc1Inv<T>& inv, int iter, T h, const Sfc1Logs<T, R>& lg, T ur,
+                 T mpe, T& moz, int& mozsgn, T& fm, T& fh, T& fm2, T& fh2, T& cm, T& ch, T& fv) {
   typedef Mth<T, R> M;
   T mozold = moz;
   const T tmpcm = lg.tmpcm, tmpch = lg.tmpch, tmpcm2 = lg.tmpcm2, tmpch2 = lg.tmpch2;
@@ -233,12 +256,11 @@ DEV void sfcdif1(int iter, T sfctmp, T rhoair, T h, T qair, T zlvl, T zpd, const
     moz = L(0.0);
     moz2 = L(0.0);
   } else {
-    T tvir = (L(1.0) + L(0.61) * qair) * sfctmp;
-    T tmp1 = dv(KARMAN * dv(GRAV, tvir) * h, rhoair * CPAIR);
+    T tmp1 = d.div(inv.kgtv * h, inv.rhocp);
     if (fabs(tmp1) <= mpe) tmp1 = mpe;
-    T mol = dv(L(-1.0) * p3(fv), tmp1);
-    moz = rmin(dv(zlvl - zpd, mol), L(1.0));
-    moz2 = rmin(dv(L(2.0) + z0h, mol), L(1.0));
+    const Recip<T> rmol = d.rec(d.div(L(-1.0) * p3(fv), d.rec(tmp1)));
+    moz = rmin(d.divk(inv.dz, rmol), L(1.0));
+    moz2 = rmin(d.divk(inv.d2, rmol), L(1.0));
   }
   if (mozold * moz < L(0.0)) mozsgn = mozsgn + 1;
   if (mozsgn >= 2) {
@@ -290,8 +312,8 @@ DEV void sfcdif1(int iter, T sfctmp, T rhoair, T h, T qair, T zlvl, T zpd, const
   if (fabs(chfh) <= mpe) chfh = mpe;
   if (fabs(cm2fm2) <= mpe) cm2fm2 = mpe;
   if (fabs(ch2fh2) <= mpe) ch2fh2 = mpe;
-  cm = dv(KARMAN * KARMAN, cmfm * cmfm);
-  ch = dv(KARMAN * KARMAN, cmfm * chfh);
+  cm = d.divk(KARMAN * KARMAN, d.rec(cmfm * cmfm));
+  ch = d.divk(KARMAN * KARMAN, d.rec(cmfm * chfh));
   fv = ur * M::sqrt(cm);
 }
 
@@ -373,54 +395,31 @@ DEV void sfcdif2(int iter, T z0, T thz0, T thlm, T sfcspd, T czil, T zlm, T& akm
 }
 
 // ragrb: func.f90:3260-3350
-// Optional value dump of one column (build with -DNMP_DEBUG_DUMP; tools only,
-// tools/mcse_probe.py): NMP_DBG(i, v) stores v into nmp_dbg[i] when the lane
-// steps column nmp_dbg_col.  Compiled out otherwise.
-#ifdef NMP_DEBUG_DUMP
-static __device__ double nmp_dbg[256];
-static __device__ long long nmp_dbg_col = -1;
-#define NMP_DBG_ARG , bool dbg_lane
-#define NMP_DBG_PASS , dbg_lane
-#else
-#define NMP_DBG_ARG
-#define NMP_DBG_PASS
-#endif
-#ifdef NMP_DEBUG_DUMP
-#define NMP_DBG(i, v)                        \
-  do {                                       \
-    if (dbg_lane) nmp_dbg[i] = (double)(v);  \
-  } while (0)
-#else
-#define NMP_DBG(i, v) ((void)0)
-#endif
 
-template <class T, bool R>
-DEV void ragrb(T sqrt_dleaf_uc, int iter, T vai, T rhoair, T hg, T tah, T zpd, T z0mg, T z0hg,
-               T hcan, T z0h, T fv, T cwp, T mpe, T& fhg, T& rahg, T& rb NMP_DBG_ARG) {
+// rhocp = d.rec(RHOAIR*CPAIR), rhcan = d.rec(HCAN) and dzg = ZPD-Z0MG
+// (d.chk) are loop-invariant and formed once by the caller.
+template <class T, bool R, class D>
+DEV void ragrb(D& d, const Recip<T>& rhocp, const Recip<T>& rhcan, T dzg, T sqrt_dleaf_uc,
+               int iter, T vai, T hg, T tah, T zpd, T z0hg, T hcan, T z0h, T fv, T cwp, T mpe,
+               T& fhg, T& rahg, T& rb) {
   typedef Mth<T, R> M;
   T mozg = L(0.0);
   if (iter > 1) {
-    T tmp1 = dv(KARMAN * dv(GRAV, tah) * hg, rhoair * CPAIR);
+    T tmp1 = d.div(KARMAN * d.divk(GRAV, d.rec(tah)) * hg, rhocp);
     if (fabs(tmp1) <= mpe) tmp1 = mpe;
-    T molg = dv(L(-1.) * p3(fv), tmp1);
-    mozg = rmin(dv(zpd - z0mg, molg), L(1.0));
+    const T molg = d.div(L(-1.) * p3(fv), d.rec(tmp1));
+    mozg = rmin(d.divk(dzg, d.rec(molg)), L(1.0));
   }
   T fhgnew = (mozg < L(0.0)) ? M::pow_mq(L(1.0) - L(15.0) * mozg) : L(1.0) + L(4.7) * mozg;
   fhg = (iter == 1) ? fhgnew : L(0.5) * (fhg + fhgnew);
   T cwpc = M::sqrt(cwp * vai * hcan * fhg);
-  T tmp1 = M::exp(dv(-cwpc * z0hg, hcan));
-  T tmp2 = M::exp(dv(-cwpc * (z0h + zpd), hcan));
-  T tmprah2 = dv(hcan * M::exp(cwpc), cwpc) * (tmp1 - tmp2);
+  T tmp1 = M::exp(d.div(-cwpc * z0hg, rhcan));
+  T tmp2 = M::exp(d.div(-cwpc * (z0h + zpd), rhcan));
+  T tmprah2 = d.div(hcan * M::exp(cwpc), d.rec(cwpc)) * (tmp1 - tmp2);
   T kh = rmax(KARMAN * fv * (hcan - zpd), mpe);
-  rahg = dv(tmprah2, kh);
-  T tmprb = dv(cwpc * L(50.0), L(1.0) - M::exp(-cwpc / L(2.0)));
+  rahg = d.div(tmprah2, d.rec(kh));
+  T tmprb = d.div(cwpc * L(50.0), d.rec(L(1.0) - M::exp(-cwpc / L(2.0))));
   rb = tmprb * sqrt_dleaf_uc;
-  if (iter == 1) {
-    NMP_DBG(208, hcan); NMP_DBG(209, zpd); NMP_DBG(210, z0mg); NMP_DBG(211, z0h);
-    NMP_DBG(212, fv); NMP_DBG(213, vai); NMP_DBG(214, cwp); NMP_DBG(215, cwpc);
-    NMP_DBG(216, tmp1); NMP_DBG(217, tmp2); NMP_DBG(218, tmprah2); NMP_DBG(219, kh);
-    NMP_DBG(220, rahg); NMP_DBG(221, tmprb); NMP_DBG(222, fhg); NMP_DBG(223, z0hg);
-  }
 }
 
 // stomata (Ball-Berry bisection): func.f90:3739-3887
@@ -803,6 +802,10 @@ DEV void gst(T* p, T v) {
   else *p = v;
 }
 
+// lanes of all launches that re-ran the canopy loop with the reference's
+// divisions (DivFast32 guard failed); read and reset by nmp_div_redo_count
+static __device__ unsigned long long nmp_div_redo;
+
 template <class T>
 struct Sink {
   T* dg;        // diag + column (NULL when level == NMP_DIAG_NONE)
@@ -842,6 +845,9 @@ struct Sink {
   }
   DEV void s(int f, T v) const { gst(st + f * ld, v); }
   DEV void isn(int v) const { gst(isnow, (int32_t)v); }
+  // a lane that re-ran the canopy Newton loop with the reference's divisions
+  // (the fast division's guard failed; nmp_engine_info's counter, tests)
+  static DEV void count_redo() { atomicAdd(&nmp_div_redo, 1ull); }
   // re-binning key: the vege_flux Newton trip count of this step (0 = no canopy)
   DEV void trips(int n) const {
     if (cost) *cost = (uint8_t)n;
@@ -931,6 +937,15 @@ static __device__ unsigned long long nmp_wave_rec[4 * NMP_WAVE_REC_MAX];
 static __device__ unsigned int nmp_wave_ctr;
 #endif
 
+// The canopy Newton loop's fp32 divisions through DivFast32 (sflx_math.h):
+// the "ref" fp32 kernels; NMP_FAST_DIV=0 keeps the reference's IEEE sequence
+// (A/B only, results identical).
+#ifndef NMP_FAST_DIV
+#define NMP_FAST_DIV 1
+#endif
+template <class T, bool R>
+constexpr bool kFastDiv = NMP_FAST_DIV != 0 && sizeof(T) == 4 && R;
+
 // Unroll factor of the vege_flux Newton loop (tuning knob, results identical).
 #ifndef NMP_VEGE_UNROLL
 #define NMP_VEGE_UNROLL 1
@@ -958,12 +973,16 @@ constexpr Opt kOptionSet[3] = {{1, 1, 1, 1, 1, 1, 1, 1, 2, 1, 1, 1},
                                {1, 1, 1, 1, 1, 1, 1, 1, 2, 1, 1, 1},
                                {2, 1, 1, 1, 1, 1, 1, 1, 2, 1, 1, 1}};
 
-template <class T, bool R, int OS>
-DEV void sflx_column(const DevParams& P, const KArgs<T>& A, Col<T>& c, const Sink<T>& out) {
+// FD: the canopy Newton loop divides with DivFast32 (sflx_math.h) where the
+// policy allows it (kFastDiv).  Such a call returns false -- with nothing
+// stored that the column's re-run reads -- when any canopy lane of the wave
+// left the fast division's exact range; the caller then steps the wave's
+// columns again with FD = false (column_ref).  Otherwise it returns true.
+template <class T, bool R, int OS, bool FD>
+DEV bool sflx_column(const DevParams& P, const KArgs<T>& A, Col<T>& c, const Sink<T>& out) {
   typedef Mth<T, R> M;
-#ifdef NMP_DEBUG_DUMP
-  const bool dbg_lane = (long long)(out.st - A.state) == nmp_dbg_col;
-#endif
+  constexpr bool kFD = FD && kFastDiv<T, R>;
+
 #ifdef NMP_PHASE_TIMING
   PhaseClock pclk{__builtin_amdgcn_s_memtime(), 0};
 #endif
@@ -1020,7 +1039,10 @@ DEV void sflx_column(const DevParams& P, const KArgs<T>& A, Col<T>& c, const Sin
     c.lai = L(0.0);
     c.sai = L(0.0);
   }
-  if (!(o.veg == 2 || o.veg == 5)) {  // no carbon model: LAI/SAI are final here
+  // no carbon model: LAI/SAI are final here.  (Storing them before a
+  // fast-division re-run is safe: for opt_veg 1/3/4 they are the table's
+  // values above, whatever the stored ones were.)
+  if (!(o.veg == 2 || o.veg == 5)) {
     out.s(NMP_S_LAI, c.lai);
     out.s(NMP_S_SAI, c.sai);
   }
@@ -1194,8 +1216,10 @@ DEV void sflx_column(const DevParams& P, const KArgs<T>& A, Col<T>& c, const Sin
     fsun = (L(1.0) - M::exp(-ext * vaia)) / rmax(ext * vaia, mpe6);
     ext = fsun;
     fsun = (ext < L(0.01)) ? L(0.) : ext;
-    out.s(NMP_S_ALBOLD, c.albold);
-    out.s(NMP_S_TAUSS, c.tauss);
+    if constexpr (!kFD) {
+      out.s(NMP_S_ALBOLD, c.albold);
+      out.s(NMP_S_TAUSS, c.tauss);
+    }
   }
   T fsha = L(1.0) - fsun;
   T laisun = elai * fsun;
@@ -1293,8 +1317,8 @@ DEV void sflx_column(const DevParams& P, const KArgs<T>& A, Col<T>& c, const Sin
   }
   if (c.lutyp == P.g.isurban && c.snowh == L(0.0)) rsurf = L(1.0E6);
   const bool frozen_canopy = !(c.tv > TFRZ);
-  const T latheav = frozen_canopy ? HSUB : HVAP;
-  const T gammav = CPAIR * c.sfcprs / (L(0.622) * latheav);
+  T latheav = frozen_canopy ? HSUB : HVAP;
+  T gammav = CPAIR * c.sfcprs / (L(0.622) * latheav);
   const bool frozen_ground = !(c.tg > TFRZ);
   const T latheag = frozen_ground ? HSUB : HVAP;
   const T gammag = CPAIR * c.sfcprs / (L(0.622) * latheag);
@@ -1309,23 +1333,18 @@ DEV void sflx_column(const DevParams& P, const KArgs<T>& A, Col<T>& c, const Sin
   // ---- vege_flux: func.f90:2465-2964 ----
   T tgv = L(0.0), cmv = L(0.0);
   int vtrips = 0;
+  bool need_ref = false;  // this lane's canopy loop left DivFast32's range
   if (veg && fveg > L(0.0)) {
     tgv = c.tg;
-    cmv = c.cm;
-    chv = c.ch;
     const T mpe = L(1E-6);
-    int liter = 0;
-    T fv = L(0.1), h = L(0.0), hg = L(0.0);
-    int mozsgn = 0;
-    T moz = L(0.0), fm = L(0.0), fh = L(0.0), fm2 = L(0.0), fh2 = L(0.0);
-    T fhg = L(0.0), wstar = L(0.0), rahg = L(0.0), rb = L(0.0), cah = L(0.0), cvh = L(0.0);
+    T fv, h, hg, moz, fm, fh, fm2, fh2, fhg, wstar, rahg, rb, rahc, cah, cvh;
+    int mozsgn;
     T z0h = z0m;
     T vaie = rmin(L(6.0), vai / fveg);
     T laisune = rmin(L(6.0), laisun / fveg);
     T laishae = rmin(L(6.0), laisha / fveg);
-    T tt = tdc(tgv);
-    T estg = esat_val(tt);
-    c.qsfc = L(0.622) * eair / (c.psfc - L(0.378) * eair);
+    T tt;
+    T estg = esat_val(tdc(tgv));
     T hcan = htop;
     // HCAN = HVT and Z0M = Z0MVT here: LOG(HCAN/Z0M) is veg-type-only
     T uc = ur * ((sizeof(T) == 4 && R) ? (T)V.log_hvt_z0m : M::log(hcan / z0m)) / M::log(zlvl / z0m);
@@ -1333,41 +1352,57 @@ DEV void sflx_column(const DevParams& P, const KArgs<T>& A, Col<T>& c, const Sin
     T air = -emv * (L(1.0) + (L(1.0) - emv) * (L(1.0) - emg)) * c.lwdn -
             emv * emg * SB * p4(tgv);
     T cir = (L(2.0) - emv * (L(1.0) - emg)) * emv * SB;
-    T rahc = L(1.0);
-    const T sqrt_dleaf_uc = M::sqrt((T)V.dleaf / uc);  // ragrb :3349, loop-invariant
+    T sqrt_dleaf_uc = M::sqrt((T)V.dleaf / uc);  // ragrb :3349, loop-invariant
     const T log_2z0m_v = (T)V.log_2z0m;  // Z0M = Z0MVT: veg-type-only
-    const Sfc1Logs<T, R> lgv =
+    Sfc1Logs<T, R> lgv =
         (o.sfc == 1) ? Sfc1Logs<T, R>(zlvl, zpd, z0m, z0h, c.status,
                                       (sizeof(T) == 4 && R) ? &log_2z0m_v : nullptr)
                      : Sfc1Logs<T, R>{};
-#ifndef NMP_VEGE_NOPEEL
-    // One Newton iteration (loop1, func.f90:2744-2877).  Iteration 1 is peeled
-    // (it alone calls stomata/canres, :2779-2803), so the loop that runs the
-    // remaining iterations carries none of stomata's code or registers.
-    auto vege_iter = [&](const int iter, auto first) -> T {
-      if constexpr (!decltype(first)::value) __builtin_assume(iter >= 2);
+    // EVC's limit CANLIQ*LATHEAV/DT or CANICE*LATHEAV/DT (:2860-2864): both
+    // loop-invariant, the iteration picks one by the canopy temperature
+    T evlim_liq = dv(c.canliq * latheav, DT), evlim_ice = dv(c.canice * latheav, DT);
+    // The whole canopy Newton loop (loop1, func.f90:2744-2877) with the
+    // division policy `d` (sflx_math.h): every loop variable starts here, so a
+    // lane can run it again with the reference's divisions.
+    auto vege_loop = [&](auto& d) {
+      cmv = c.cm;
+      chv = c.ch;
+      fv = L(0.1); h = L(0.0); hg = L(0.0);
+      mozsgn = 0;
+      moz = fm = fh = fm2 = fh2 = L(0.0);
+      fhg = wstar = rahg = rb = cah = cvh = L(0.0);
+      rahc = L(1.0);
+      c.qsfc = L(0.622) * eair / (c.psfc - L(0.378) * eair);
+      int liter = 0;
+      // loop-invariant operands of the divisions (same values as the
+      // reference forms in every iteration)
+      const Sfc1Inv<T> inv = sfc1_inv(d, c.sfctmp, qair, rhoair, zlvl, zpd, z0h);
+      const Recip<T> rhcan = d.rec(hcan), rgammav = d.rec(gammav);
+      const T dzg = zpd - z0mg, two_vaie = L(2.0) * vaie, fwet_vaie = c.fwet * vaie;
+      d.chk(dzg);
+      d.chk(two_vaie);
+      d.chk(fwet_vaie);
+      d.chk(laisune);
+      d.chk(laishae);
+      // One Newton iteration.  Iteration 1 is peeled (it alone calls
+      // stomata/canres, :2779-2803), so the loop that runs the remaining
+      // iterations carries none of stomata's code or registers.
+      auto vege_iter = [&](const int iter, auto first) -> T {
+        if constexpr (!decltype(first)::value) __builtin_assume(iter >= 2);
         if (o.sfc == 1)
-          sfcdif1<T, R>(iter, c.sfctmp, rhoair, h, qair, zlvl, zpd, lgv, z0h, ur, mpe, moz, mozsgn,
-                        fm, fh, fm2, fh2, cmv, chv, fv);
+          sfcdif1<T, R>(d, inv, iter, h, lgv, ur, mpe, moz, mozsgn, fm, fh, fm2, fh2, cmv, chv, fv);
         if (o.sfc == 2) {
           sfcdif2<T, R>(iter, z0m, c.tah, thair, ur, (T)P.g.czil, zlvl, cmv, chv, moz, wstar, fv);
           chv = chv / ur;
           cmv = cmv / ur;
         }
-        const int dbi = (iter <= 3 ? iter - 1 : 3) * 40;
-        NMP_DBG(dbi + 0, moz); NMP_DBG(dbi + 1, fm); NMP_DBG(dbi + 2, fh);
-        NMP_DBG(dbi + 3, cmv); NMP_DBG(dbi + 4, chv); NMP_DBG(dbi + 5, fv);
-        rahc = rmax(L(1.0), dv(L(1.0), chv * ur));
-        NMP_DBG(dbi + 6, rahc);
-        T rawc = rahc;
-        ragrb<T, R>(sqrt_dleaf_uc, iter, vaie, rhoair, hg, c.tah, zpd, z0mg, z0mg, hcan, z0h, fv,
-                    cwp, mpe, fhg, rahg, rb NMP_DBG_PASS);
-        NMP_DBG(dbi + 7, fhg); NMP_DBG(dbi + 8, rahg); NMP_DBG(dbi + 9, rb);
-        T rawg = rahg;
-        tt = tdc(c.tv);
+        rahc = rmax(L(1.0), d.divk(L(1.0), d.rec(chv * ur)));
+        const Recip<T> rrahc = d.rec(rahc);  // RAWC = RAHC: CAH = CAW, H share it
+        ragrb<T, R>(d, inv.rhocp, rhcan, dzg, sqrt_dleaf_uc, iter, vaie, hg, c.tah, zpd, z0mg, hcan,
+                    z0h, fv, cwp, mpe, fhg, rahg, rb);
+        const Recip<T> rrahg = d.rec(rahg), rrb = d.rec(rb);  // RAWG = RAHG
         T estv, destv;
-        esat_sel(tt, estv, destv);
-        NMP_DBG(dbi + 10, estv); NMP_DBG(dbi + 11, destv);
+        esat_sel(tdc(c.tv), estv, destv);
         if constexpr (decltype(first)::value) {  // iter == 1
           if (o.crs == 1) {
             const StomataPre<T> sp =
@@ -1381,138 +1416,64 @@ DEV void sflx_column(const DevParams& P, const KArgs<T>& A, Col<T>& c, const Sin
             canres<T, R>(V, c.sfcprs, c.tv, parsha, c.eah, btran, rssha, psnsha);
           }
         }
-        cah = dv(L(1.0), rahc);
-        cvh = dv(L(2.0) * vaie, rb);
-        T cgh = dv(L(1.0), rahg);
+        cah = d.divk(L(1.0), rrahc);
+        cvh = d.divk(two_vaie, rrb);
+        T cgh = d.divk(L(1.0), rrahg);
         T cond = cah + cvh + cgh;
-        T ata = dv(c.sfctmp * cah + tgv * cgh, cond);
-        T bta = dv(cvh, cond);
+        const Recip<T> rcond = d.rec(cond);
+        T ata = d.div(c.sfctmp * cah + tgv * cgh, rcond);
+        T bta = d.div(cvh, rcond);
         T csh = (L(1.0) - bta) * rhoair * CPAIR * cvh;
-        T caw = dv(L(1.0), rawc);
-        T cew = dv(c.fwet * vaie, rb);
-        T ctw = (L(1.0) - c.fwet) * (dv(laisune, rb + rssun) + dv(laishae, rb + rssha));
-        T cgw = dv(L(1.0), rawg + rsurf);
+        T caw = d.divk(L(1.0), rrahc);
+        T cew = d.divk(fwet_vaie, rrb);
+        T ctw = (L(1.0) - c.fwet) *
+                (d.divk(laisune, d.rec(rb + rssun)) + d.divk(laishae, d.rec(rb + rssha)));
+        T cgw = d.divk(L(1.0), d.rec(rahg + rsurf));
         cond = caw + cew + ctw + cgw;
-        T aea = dv(eair * caw + estg * cgw, cond);
-        T bea = dv(cew + ctw, cond);
-        T cev = dv((L(1.0) - bea) * cew * rhoair * CPAIR, gammav);
-        T ctr = dv((L(1.0) - bea) * ctw * rhoair * CPAIR, gammav);
-        NMP_DBG(dbi + 12, cah); NMP_DBG(dbi + 13, cvh); NMP_DBG(dbi + 14, cgh);
-        NMP_DBG(dbi + 15, ata); NMP_DBG(dbi + 16, bta); NMP_DBG(dbi + 17, caw);
-        NMP_DBG(dbi + 18, cew); NMP_DBG(dbi + 19, ctw); NMP_DBG(dbi + 20, cgw);
-        NMP_DBG(dbi + 21, aea); NMP_DBG(dbi + 22, bea); NMP_DBG(dbi + 23, cev);
-        NMP_DBG(dbi + 24, ctr); NMP_DBG(dbi + 25, rssun); NMP_DBG(dbi + 26, rssha);
+        const Recip<T> rcond2 = d.rec(cond);
+        T aea = d.div(eair * caw + estg * cgw, rcond2);
+        T bea = d.div(cew + ctw, rcond2);
+        T cev = d.div((L(1.0) - bea) * cew * rhoair * CPAIR, rgammav);
+        T ctr = d.div((L(1.0) - bea) * ctw * rhoair * CPAIR, rgammav);
         c.tah = ata + bta * c.tv;
         c.eah = aea + bea * estv;
         irc = fveg * (air + cir * p4(c.tv));
         shc = fveg * rhoair * CPAIR * cvh * (c.tv - c.tah);
-        evc = dv(fveg * rhoair * CPAIR * cew * (estv - c.eah), gammav);
-        tr = dv(fveg * rhoair * CPAIR * ctw * (estv - c.eah), gammav);
-        if (c.tv > TFRZ)
-          evc = rmin(dv(c.canliq * latheav, DT), evc);
-        else
-          evc = rmin(dv(c.canice * latheav, DT), evc);
+        evc = d.div(fveg * rhoair * CPAIR * cew * (estv - c.eah), rgammav);
+        tr = d.div(fveg * rhoair * CPAIR * ctw * (estv - c.eah), rgammav);
+        evc = rmin((c.tv > TFRZ) ? evlim_liq : evlim_ice, evc);
         T b = sav - irc - shc - evc - tr;
         T a = fveg * (L(4.0) * cir * p3(c.tv) + csh + (cev + ctr) * destv);
-        T dtv = dv(b, a);
+        T dtv = d.div(b, d.rec(a));
         irc = irc + fveg * L(4.0) * cir * p3(c.tv) * dtv;
         shc = shc + fveg * csh * dtv;
         evc = evc + fveg * cev * destv * dtv;
         tr = tr + fveg * ctr * destv * dtv;
         c.tv = c.tv + dtv;
-        h = dv(rhoair * CPAIR * (c.tah - c.sfctmp), rahc);
-        hg = dv(rhoair * CPAIR * (tgv - c.tah), rahg);
-        c.qsfc = dv(L(0.622) * c.eah, c.sfcprs - L(0.378) * c.eah);
-        NMP_DBG(dbi + 27, c.tah); NMP_DBG(dbi + 28, c.eah); NMP_DBG(dbi + 29, irc);
-        NMP_DBG(dbi + 30, shc); NMP_DBG(dbi + 31, evc); NMP_DBG(dbi + 32, tr);
-        NMP_DBG(dbi + 33, dtv); NMP_DBG(dbi + 34, c.tv); NMP_DBG(dbi + 35, h);
-        NMP_DBG(dbi + 36, hg); NMP_DBG(dbi + 37, c.qsfc); NMP_DBG(dbi + 38, sav);
-        NMP_DBG(dbi + 39, a);
+        h = d.div(rhoair * CPAIR * (c.tah - c.sfctmp), rrahc);
+        hg = d.div(rhoair * CPAIR * (tgv - c.tah), rrahg);
+        c.qsfc = d.div(L(0.622) * c.eah, d.rec(c.sfcprs - L(0.378) * c.eah));
         return dtv;
+      };
+      vtrips = 1;
+      vege_iter(1, std::true_type{});  // iter 1 cannot exit (the test needs iter >= 5)
+      NMP_UNROLL(NMP_VEGE_UNROLL)
+      for (int iter = 2; iter <= 20; ++iter) {
+        vtrips = iter;
+        const T dtv = vege_iter(iter, std::false_type{});
+        if (liter == 1) break;
+        if (iter >= 5 && fabs(dtv) <= L(0.01) && liter == 0) liter = 1;
+      }
     };
-    vtrips = 1;
-    vege_iter(1, std::true_type{});  // iter 1 cannot exit (the test needs iter >= 5)
-    NMP_UNROLL(NMP_VEGE_UNROLL)
-    for (int iter = 2; iter <= 20; ++iter) {
-      vtrips = iter;
-      const T dtv = vege_iter(iter, std::false_type{});
-      if (liter == 1) break;
-      if (iter >= 5 && fabs(dtv) <= L(0.01) && liter == 0) liter = 1;
+    if constexpr (kFD) {
+      DivFast32 df;
+      vege_loop(df);
+      // (probes: NMP_FAST_DIV 2 = never re-run (timing), 3 = always)
+      need_ref = NMP_FAST_DIV == 3 || (NMP_FAST_DIV != 2 && !df.ok());
+    } else {
+      DivRef<T> dr;
+      vege_loop(dr);
     }
-#else
-#pragma unroll 1
-    for (int iter = 1; iter <= 20; ++iter) {
-      vtrips = iter;
-      if (o.sfc == 1)
-        sfcdif1<T, R>(iter, c.sfctmp, rhoair, h, qair, zlvl, zpd, lgv, z0h, ur, mpe, moz, mozsgn,
-                      fm, fh, fm2, fh2, cmv, chv, fv);
-      if (o.sfc == 2) {
-        sfcdif2<T, R>(iter, z0m, c.tah, thair, ur, (T)P.g.czil, zlvl, cmv, chv, moz, wstar, fv);
-        chv = chv / ur;
-        cmv = cmv / ur;
-      }
-      rahc = rmax(L(1.0), L(1.0) / (chv * ur));
-      T rawc = rahc;
-      ragrb<T, R>(sqrt_dleaf_uc, iter, vaie, rhoair, hg, c.tah, zpd, z0mg, z0mg, hcan, z0h, fv,
-                  cwp, mpe, fhg, rahg, rb NMP_DBG_PASS);
-      T rawg = rahg;
-      tt = tdc(c.tv);
-      T estv, destv;
-      esat_sel(tt, estv, destv);
-      if (iter == 1) {
-        if (o.crs == 1) {
-          const StomataPre<T> sp =
-              stomata_pre<T, R>(V, parsun > L(0.0) || parsha > L(0.0), c.sfcprs, c.sfctmp, c.tv,
-                                c.o2air, c.foln, btran, rb);
-          stomata_solve<T, R>(V, sp, igs, c.sfcprs, parsun, c.eah, estv, c.co2air, rssun, psnsun);
-          stomata_solve<T, R>(V, sp, igs, c.sfcprs, parsha, c.eah, estv, c.co2air, rssha, psnsha);
-        }
-        if (o.crs == 2) {
-          canres<T, R>(V, c.sfcprs, c.tv, parsun, c.eah, btran, rssun, psnsun);
-          canres<T, R>(V, c.sfcprs, c.tv, parsha, c.eah, btran, rssha, psnsha);
-        }
-      }
-      cah = L(1.0) / rahc;
-      cvh = L(2.0) * vaie / rb;
-      T cgh = L(1.0) / rahg;
-      T cond = cah + cvh + cgh;
-      T ata = (c.sfctmp * cah + tgv * cgh) / cond;
-      T bta = cvh / cond;
-      T csh = (L(1.0) - bta) * rhoair * CPAIR * cvh;
-      T caw = L(1.0) / rawc;
-      T cew = c.fwet * vaie / rb;
-      T ctw = (L(1.0) - c.fwet) * (laisune / (rb + rssun) + laishae / (rb + rssha));
-      T cgw = L(1.0) / (rawg + rsurf);
-      cond = caw + cew + ctw + cgw;
-      T aea = (eair * caw + estg * cgw) / cond;
-      T bea = (cew + ctw) / cond;
-      T cev = (L(1.0) - bea) * cew * rhoair * CPAIR / gammav;
-      T ctr = (L(1.0) - bea) * ctw * rhoair * CPAIR / gammav;
-      c.tah = ata + bta * c.tv;
-      c.eah = aea + bea * estv;
-      irc = fveg * (air + cir * p4(c.tv));
-      shc = fveg * rhoair * CPAIR * cvh * (c.tv - c.tah);
-      evc = fveg * rhoair * CPAIR * cew * (estv - c.eah) / gammav;
-      tr = fveg * rhoair * CPAIR * ctw * (estv - c.eah) / gammav;
-      if (c.tv > TFRZ)
-        evc = rmin(c.canliq * latheav / DT, evc);
-      else
-        evc = rmin(c.canice * latheav / DT, evc);
-      T b = sav - irc - shc - evc - tr;
-      T a = fveg * (L(4.0) * cir * p3(c.tv) + csh + (cev + ctr) * destv);
-      T dtv = b / a;
-      irc = irc + fveg * L(4.0) * cir * p3(c.tv) * dtv;
-      shc = shc + fveg * csh * dtv;
-      evc = evc + fveg * cev * destv * dtv;
-      tr = tr + fveg * ctr * destv * dtv;
-      c.tv = c.tv + dtv;
-      h = rhoair * CPAIR * (c.tah - c.sfctmp) / rahc;
-      hg = rhoair * CPAIR * (tgv - c.tah) / rahg;
-      c.qsfc = (L(0.622) * c.eah) / (c.sfcprs - L(0.378) * c.eah);
-      if (liter == 1) break;
-      if (iter >= 5 && fabs(dtv) <= L(0.01) && liter == 0) liter = 1;
-    }
-#endif
     // under-canopy fluxes and TG (loop2, :2881-2914)
     air = -emg * (L(1.0) - emv) * c.lwdn - emg * emv * SB * p4(c.tv);
     cir = emg * SB;
@@ -1558,6 +1519,16 @@ NMP_UNROLL(NMP_LOOP2_UNROLL)
     chleaf = cvh;
     chuc = L(1.0) / rahg;
   }
+  if constexpr (kFD) {
+    // every lane of the wave is active again here: a wave-uniform decision.
+    // Nothing the re-run reads has been stored yet (the diagnostics written so
+    // far are rewritten with the same values; ALBOLD/TAUSS were held back).
+    if (__builtin_amdgcn_ballot_w64(need_ref) != 0) return false;
+    if (c.cosz > L(0.0)) {
+      out.s(NMP_S_ALBOLD, c.albold);
+      out.s(NMP_S_TAUSS, c.tauss);
+    }
+  }
   out.trips(vtrips);
 
   NMP_PHASE(5);
@@ -1580,11 +1551,12 @@ NMP_UNROLL(NMP_LOOP2_UNROLL)
     irb = shb = evb = ghb = L(0.0);
     const Sfc1Logs<T, R> lgb = (o.sfc == 1) ? Sfc1Logs<T, R>(zlvl, zpdg, z0mg, z0h, c.status)
                                             : Sfc1Logs<T, R>{};
+    DivRef<T> drb;  // bare_flux keeps the reference's divisions
+    const Sfc1Inv<T> invb = sfc1_inv(drb, c.sfctmp, qair, rhoair, zlvl, zpdg, z0h);
 NMP_UNROLL(kBareUnroll)
     for (int iter = 1; iter <= 5; ++iter) {
       if (o.sfc == 1)
-        sfcdif1<T, R>(iter, c.sfctmp, rhoair, h, qair, zlvl, zpdg, lgb, z0h, ur, mpe, moz,
-                      mozsgn, fm, fh, fm2, fh2, cmb, chb, fv);
+        sfcdif1<T, R>(drb, invb, iter, h, lgb, ur, mpe, moz, mozsgn, fm, fh, fm2, fh2, cmb, chb, fv);
       if (o.sfc == 2) {
         sfcdif2<T, R>(iter, z0mg, tgb, thair, ur, (T)P.g.czil, zlvl, cmb, chb, moz, wstar, fv);
         chb = chb / ur;
@@ -2023,7 +1995,7 @@ NMP_UNROLL(kBareUnroll)
   out.template d<NMP_D_EDIR>(edir);
   out.s(NMP_S_SNEQVO, c.sneqvo);
 #ifdef NMP_TRUNC_ENERGY
-  return;  // timing experiment only (tools/build_variants.py): the energy phase alone
+  return true;  // timing experiment only (tools/build_variants.py): the energy phase alone
 #endif
 
   NMP_PHASE(9);
@@ -2576,21 +2548,7 @@ NMP_UNROLL(kBareUnroll)
         pp[k] = L(0.);
         del[k] = L(0.);
       }
-      if (it == 1) {
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          NMP_DBG(160 + k, wdf[k]); NMP_DBG(164 + k, wcnd[k]); NMP_DBG(168 + k, ai[k]);
-          NMP_DBG(172 + k, bi[k]); NMP_DBG(176 + k, ci[k]); NMP_DBG(180 + k, rhstt[k]);
-          NMP_DBG(184 + k, c.sh2o[k]); NMP_DBG(188 + k, etrani[k]); NMP_DBG(196 + k, c.smc[k]);
-        }
-        NMP_DBG(200, qinfil); NMP_DBG(201, qseva); NMP_DBG(202, qinsrf); NMP_DBG(203, dtfine);
-        NMP_DBG(204, (T)niter); NMP_DBG(205, smcmax); NMP_DBG(206, bexp); NMP_DBG(207, dwsat);
-      }
       rosr12<T, 4>(pp, ai, bi, ciin, rin, del, 0);
-      if (it == 1) {
-#pragma unroll
-        for (int k = 0; k < 4; ++k) NMP_DBG(192 + k, pp[k]);
-      }
 #pragma unroll
       for (int k = 0; k < 4; ++k) c.sh2o[k] = c.sh2o[k] + pp[k];
       T wplus = L(0.0);
@@ -2852,6 +2810,7 @@ NMP_UNROLL(kBareUnroll)
   out.template d<NMP_D_Q2B>(q2b);
   out.s(NMP_S_QSFC, c.qsfc); out.s(NMP_S_SNOWH, c.snowh); out.s(NMP_S_SNEQV, c.sneqv);
   NMP_PHASE(15);
+  return true;
 }
 
 // ---------------------------------------------------------------------------
@@ -2876,6 +2835,75 @@ constexpr int waves_per_eu(bool small) {
   return sizeof(T) == 4 ? (small ? NMP_WAVES_PER_EU / 2 : NMP_WAVES_PER_EU)
                         : (small ? (NMP_WAVES_PER_EU_F64 + 1) / 2 : NMP_WAVES_PER_EU_F64);
 }
+// the LDS layer copy's completion is explicit: LDS-DMA loads count in
+// vmcnt, and the "memory" clobber keeps every LDS read of the copied fields
+// (NMP_LOAD_COLUMN and the re-read after the flux loops, Sink::fresh_state)
+// below the wait
+template <class T, bool R>
+DEV void lds_copy_wait() {
+#if NMP_LDS_EXPLICIT_WAIT
+  if constexpr (kPrefetch<T, R>) __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
+}
+
+// The loads of column c0 into `Col<T> c` and the column's output sink `out`,
+// declared in the enclosing scope.  The layer state comes from the
+// workgroup's LDS copy when kPrefetch (issued by the kernel), the other
+// fields from HBM; ALBOLD/TAUSS/QSNOW/SNEQVO are loaded where used (the
+// daylight radiation block), QSNOW and SNEQVO reassigned before the water
+// phase reads them.  A macro, not a function: the kernel body inlined through
+// one more function level compiles to a different schedule, with 61 -> 101
+// spilled VGPRs (fp32 run-time math) and 31 -> 79 (fp64).
+#define NMP_LOAD_COLUMN(T, R)                                                                \
+  Col<T> c;                                                                                  \
+  const int64_t ld = a.ld;                                                                   \
+  const T* st = a.state + c0;                                                                \
+  c.tv = gld(st + NMP_S_TV * ld); c.tg = gld(st + NMP_S_TG * ld);                            \
+  c.fwet = gld(st + NMP_S_FWET * ld); c.snowh = gld(st + NMP_S_SNOWH * ld);                  \
+  c.sneqv = gld(st + NMP_S_SNEQV * ld);                                                      \
+  c.lai = gld(st + NMP_S_LAI * ld); c.sai = gld(st + NMP_S_SAI * ld);                        \
+  c.albold = c.tauss = c.qsnow = c.sneqvo = (T)0;                                            \
+  c.isnow = gld(a.isnow + c0);                                                               \
+  const T* sf = a.static_f + c0;                                                             \
+  c.lat = gld(sf + NMP_F_LAT * ld); c.zref = gld(sf + NMP_F_ZLVL * ld);                      \
+  c.shdfac = gld(sf + NMP_F_SHDFAC * ld); c.shdmax = gld(sf + NMP_F_SHDMAX * ld);            \
+  const int32_t* si = a.static_i + c0;                                                       \
+  c.lutyp = gld(si + NMP_I_VEGTYP * ld); c.sltyp = gld(si + NMP_I_SOILTYP * ld);             \
+  c.isc = gld(si + NMP_I_SOILCOLOR * ld);                                                    \
+  c.ist = gld(si + NMP_I_IST * ld); c.ice = gld(si + NMP_I_ICE * ld);                        \
+  const T* fc = a.forcing + c0;                                                              \
+  c.sfctmp = gld(fc + NMP_A_SFCTMP * ld); c.sfcprs = gld(fc + NMP_A_SFCPRS * ld);            \
+  c.psfc = gld(fc + NMP_A_PSFC * ld);                                                        \
+  c.uu = gld(fc + NMP_A_UU * ld); c.vv = gld(fc + NMP_A_VV * ld);                            \
+  c.q2 = gld(fc + NMP_A_Q2 * ld);                                                            \
+  c.soldn = gld(fc + NMP_A_SOLDN * ld); c.lwdn = gld(fc + NMP_A_LWDN * ld);                  \
+  c.cosz = gld(fc + NMP_A_COSZ * ld);                                                        \
+  c.status = 0;                                                                              \
+  {                                                                                          \
+    lds_copy_wait<T, R>();                                                                   \
+    auto rd = [&](int f) -> T {                                                              \
+      if constexpr (kPfEntry<T, R>)                                                          \
+        return lds_pool()[f * NMP_BLOCK + threadIdx.x];                                      \
+      else                                                                                   \
+        return gld(st + f * ld);                                                             \
+    };                                                                                       \
+    _Pragma("unroll") for (int k = 0; k < 7; ++k) {                                          \
+      c.stc[k] = rd(NMP_S_STC + k);                                                          \
+      c.zsnso[k] = rd(NMP_S_ZSNSO + k);                                                      \
+    }                                                                                        \
+    _Pragma("unroll") for (int k = 0; k < 3; ++k) {                                          \
+      c.snice[k] = rd(NMP_S_SNICE + k);                                                      \
+      c.snliq[k] = rd(NMP_S_SNLIQ + k);                                                      \
+    }                                                                                        \
+    _Pragma("unroll") for (int k = 0; k < 4; ++k) {                                          \
+      c.sh2o[k] = rd(NMP_S_SH2O + k);                                                        \
+      c.smc[k] = rd(NMP_S_SMC + k);                                                          \
+    }                                                                                        \
+  }                                                                                          \
+  const Sink<T> out{a.diag ? a.diag + c0 : nullptr, a.state + c0, ld, a.diag_level, sf, si,  \
+                    fc, a.isnow + c0, a.cost ? a.cost + c0 : nullptr,                        \
+                    a.ficeold ? a.ficeold + c0 : nullptr}
+
 template <class T, bool R, bool SMALL, int OS>
 __global__ __launch_bounds__(NMP_BLOCK)
 __attribute__((amdgpu_waves_per_eu(waves_per_eu<T>(SMALL))))
@@ -2911,69 +2939,24 @@ void sflx_step_kernel(const DevParams* __restrict__ gparams,
   // re-binned launch: this lane steps column order[gid] (a permutation of the
   // columns; every column is independent, so results do not depend on it)
   const int64_t c0 = a.order ? (int64_t)a.order[gid] : gid;
-  const int64_t ld = a.ld;
-  Col<T> c;
-  const T* st = a.state + c0;
+  const T* st0 = a.state + c0;
   // layer state: through the LDS copy (kPrefetch) or straight from HBM.  The
   // copy is issued first; the column's other fields load while it is in flight
-  if constexpr (kPrefetch<T, R>) copy_layers_to_lds(st, ld);
-  c.tv = gld(st + NMP_S_TV * ld); c.tg = gld(st + NMP_S_TG * ld);
-  c.fwet = gld(st + NMP_S_FWET * ld); c.snowh = gld(st + NMP_S_SNOWH * ld);
-  c.sneqv = gld(st + NMP_S_SNEQV * ld);
-  c.lai = gld(st + NMP_S_LAI * ld); c.sai = gld(st + NMP_S_SAI * ld);
-  // ALBOLD/TAUSS/QSNOW/SNEQVO: loaded where used (daylight radiation block);
-  // QSNOW and SNEQVO are reassigned before the water phase reads them
-  c.albold = c.tauss = c.qsnow = c.sneqvo = (T)0;
-  c.isnow = gld(a.isnow + c0);
-  const T* sf = a.static_f + c0;
-  c.lat = gld(sf + NMP_F_LAT * ld); c.zref = gld(sf + NMP_F_ZLVL * ld); c.shdfac = gld(sf + NMP_F_SHDFAC * ld);
-  c.shdmax = gld(sf + NMP_F_SHDMAX * ld);
-  const int32_t* si = a.static_i + c0;
-  c.lutyp = gld(si + NMP_I_VEGTYP * ld); c.sltyp = gld(si + NMP_I_SOILTYP * ld);
-  c.isc = gld(si + NMP_I_SOILCOLOR * ld);
-  c.ist = gld(si + NMP_I_IST * ld); c.ice = gld(si + NMP_I_ICE * ld);
-  const T* fc = a.forcing + c0;
-  c.sfctmp = gld(fc + NMP_A_SFCTMP * ld); c.sfcprs = gld(fc + NMP_A_SFCPRS * ld); c.psfc = gld(fc + NMP_A_PSFC * ld);
-  c.uu = gld(fc + NMP_A_UU * ld); c.vv = gld(fc + NMP_A_VV * ld); c.q2 = gld(fc + NMP_A_Q2 * ld);
-  c.soldn = gld(fc + NMP_A_SOLDN * ld); c.lwdn = gld(fc + NMP_A_LWDN * ld);
-  c.cosz = gld(fc + NMP_A_COSZ * ld);
-  c.status = 0;
-  {
-    // the copy's completion is explicit: LDS-DMA loads count in vmcnt, and
-    // the "memory" clobber keeps every LDS read of the copied fields (here and
-    // the re-read after the flux loops, Sink::fresh_state) below the wait
-#if NMP_LDS_EXPLICIT_WAIT
-    if constexpr (kPrefetch<T, R>) __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#endif
-    auto rd = [&](int f) -> T {
-      if constexpr (kPfEntry<T, R>)
-        return lds_pool()[f * NMP_BLOCK + threadIdx.x];
-      else
-        return gld(st + f * ld);
-    };
-#pragma unroll
-    for (int k = 0; k < 7; ++k) {
-      c.stc[k] = rd(NMP_S_STC + k);
-      c.zsnso[k] = rd(NMP_S_ZSNSO + k);
-    }
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-      c.snice[k] = rd(NMP_S_SNICE + k);
-      c.snliq[k] = rd(NMP_S_SNLIQ + k);
-    }
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      c.sh2o[k] = rd(NMP_S_SH2O + k);
-      c.smc[k] = rd(NMP_S_SMC + k);
+  if constexpr (kPrefetch<T, R>) copy_layers_to_lds(st0, a.ld);
+  NMP_LOAD_COLUMN(T, R);
+  if (sflx_column<T, R, OS, true>(sp, a, c, out)) {
+    if (c.status != 0) a.status[c0] |= c.status;
+  } else {
+    // (kFastDiv kernels only) a canopy lane of this wave left the fast
+    // division's range: nothing is stored that a re-run reads, so the wave is
+    // queued whole for sflx_redo_kernel, launched right after this one.  One
+    // lane appends the wave's first launch index.
+    const uint64_t live = __builtin_amdgcn_read_exec();
+    if (lane == __builtin_ctzll(live)) {
+      const uint32_t i = atomicAdd(a.redo, 1u);
+      a.redo[2 + i] = (uint32_t)(gid - lane);
     }
   }
-
-  const Sink<T> out{a.diag ? a.diag + c0 : nullptr, a.state + c0, ld, a.diag_level, sf, si, fc,
-                    a.isnow + c0, a.cost ? a.cost + c0 : nullptr,
-                    a.ficeold ? a.ficeold + c0 : nullptr};
-  sflx_column<T, R, OS>(sp, a, c, out);
-
-  if (c.status != 0) a.status[c0] |= c.status;
 #ifdef NMP_WAVE_TIMING
   {
     const unsigned long long wt1 = __builtin_amdgcn_s_memrealtime();
@@ -2994,6 +2977,52 @@ void sflx_step_kernel(const DevParams* __restrict__ gparams,
 #endif
 }
 
+// The fast-division fallback: the waves the step kernel queued in a.redo
+// (redo[0] = count, redo[1] = finished workgroups, redo[2..] = each wave's
+// first launch index) stepped again with the reference's divisions.  A
+// separate kernel, because the re-run code inside the step kernel -- inlined
+// or as a call -- costs the step kernel registers on every launch (inlined:
+// 36 -> 110 spilled VGPRs; a call: 36 -> 148, and 7 % of the step).  A small
+// fixed grid; with nothing queued every workgroup returns at once.  The last
+// workgroup to finish clears the queue for the stream's next launch.
+template <class T, bool R, int OS>
+__global__ __launch_bounds__(NMP_BLOCK)
+__attribute__((amdgpu_waves_per_eu(waves_per_eu<T>(false))))
+void sflx_redo_kernel(const DevParams* __restrict__ gparams, KArgs<T> a) {
+  const uint32_t n = __hip_atomic_load(a.redo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (n == 0) return;
+  __shared__ __attribute__((aligned(16))) DevParams sp;
+  {
+    const int4* src = reinterpret_cast<const int4*>(gparams);
+    int4* dst = reinterpret_cast<int4*>(&sp);
+    constexpr int NW = sizeof(DevParams) / sizeof(int4);
+    for (int i = threadIdx.x; i < NW; i += blockDim.x) dst[i] = src[i];
+  }
+  if constexpr (sizeof(T) == 4 && R) stage_math_tables();
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const uint32_t stride = gridDim.x * (NMP_BLOCK / 64);
+  for (uint32_t j = blockIdx.x * (NMP_BLOCK / 64) + (threadIdx.x >> 6); j < n; j += stride) {
+    const int64_t gid = (int64_t)a.redo[2 + j] + lane;
+    if (lane < a.cpw && gid < a.ncol) {
+      const int64_t c0 = a.order ? (int64_t)a.order[gid] : gid;
+      if constexpr (kPrefetch<T, R>) copy_layers_to_lds(a.state + c0, a.ld);
+      NMP_LOAD_COLUMN(T, R);
+      sflx_column<T, R, OS, false>(sp, a, c, out);
+      if (c.status != 0) a.status[c0] |= c.status;
+      Sink<T>::count_redo();
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __threadfence();
+    if (atomicAdd(a.redo + 1, 1u) == gridDim.x - 1) {
+      a.redo[0] = 0u;
+      a.redo[1] = 0u;
+    }
+  }
+}
+
 // launch wrapper (one instantiation per precision / math policy)
 template <class T, bool R, bool SMALL>
 void launch_os(int os, dim3 grid, dim3 block, hipStream_t stream, const DevParams* dparams,
@@ -3004,6 +3033,19 @@ void launch_os(int os, dim3 grid, dim3 block, hipStream_t stream, const DevParam
     hipLaunchKernelGGL((sflx_step_kernel<T, R, SMALL, 2>), grid, block, 0, stream, dparams, a);
   else
     hipLaunchKernelGGL((sflx_step_kernel<T, R, SMALL, 0>), grid, block, 0, stream, dparams, a);
+}
+
+// the fast-division fallback after a step launch (kFastDiv kernels only):
+// one workgroup per 16 CUs' worth of waves -- the queue is normally empty
+template <class T, bool R>
+void launch_redo(int os, hipStream_t stream, const DevParams* dparams, const KArgs<T>& a) {
+  const dim3 grid(64), block(NMP_BLOCK);
+  if (os == 1)
+    hipLaunchKernelGGL((sflx_redo_kernel<T, R, 1>), grid, block, 0, stream, dparams, a);
+  else if (os == 2)
+    hipLaunchKernelGGL((sflx_redo_kernel<T, R, 2>), grid, block, 0, stream, dparams, a);
+  else
+    hipLaunchKernelGGL((sflx_redo_kernel<T, R, 0>), grid, block, 0, stream, dparams, a);
 }
 
 // launch wrapper (one instantiation per precision / math policy).  os: the
@@ -3017,10 +3059,12 @@ hipError_t launch_sflx(const DevParams* dparams, const KArgs<T>& a, hipStream_t 
   if (grid == 0) return hipSuccess;
   // the fast-math fp32 path has neither a small nor option-set instantiation (code size)
   if constexpr (sizeof(T) == 8 || R) {
+    if (kFastDiv<T, R> && !a.redo) return hipErrorInvalidValue;  // the fallback queue
     if (small)
       launch_os<T, R, true>(os, dim3((unsigned)grid), dim3(block), stream, dparams, a);
     else
       launch_os<T, R, false>(os, dim3((unsigned)grid), dim3(block), stream, dparams, a);
+    if constexpr (kFastDiv<T, R>) launch_redo<T, R>(os, stream, dparams, a);
   } else {
     hipLaunchKernelGGL((sflx_step_kernel<T, R, false, 0>), dim3((unsigned)grid), dim3(block), 0,
                        stream, dparams, a);
@@ -3062,19 +3106,20 @@ extern "C" int nmp_debug_phase_cycles(unsigned long long* out16, int reset) {
 #endif
 #endif
 
-#if defined(NMP_DEBUG_DUMP) && (!defined(NMP_TU) || NMP_TU == 8)
-// debug dump (tools/mcse_probe.py): col >= 0 selects the column the next launches
-// dump (and clears the buffer to NaN); out (256 doubles) receives the buffer
-extern "C" int nmp_debug_dump(long long col, double* out) {
-  if (col >= 0) {
-    double nan[256];
-    for (int i = 0; i < 256; ++i) nan[i] = __builtin_nan("");
-    if (hipMemcpyToSymbol(HIP_SYMBOL(nmp_dbg), nan, sizeof(nan)) != hipSuccess) return -4;
-    if (hipMemcpyToSymbol(HIP_SYMBOL(nmp_dbg_col), &col, sizeof(col)) != hipSuccess) return -4;
+
+#if !defined(NMP_TU) || NMP_TU == 4
+// the canopy-loop re-runs of the fp32 kernels (DivFast32's guard): the count
+// since the last reset; reset != 0 clears it afterwards
+extern "C" int nmp_div_redo_count(unsigned long long* out, int reset) {
+  if (!out) return NMP_E_ARG;
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(nmp_div_redo), sizeof(*out)) != hipSuccess)
+    return NMP_E_DEVICE;
+  if (reset) {
+    const unsigned long long z = 0;
+    if (hipMemcpyToSymbol(HIP_SYMBOL(nmp_div_redo), &z, sizeof(z)) != hipSuccess)
+      return NMP_E_DEVICE;
   }
-  if (out && hipMemcpyFromSymbol(out, HIP_SYMBOL(nmp_dbg), 256 * sizeof(double)) != hipSuccess)
-    return -4;
-  return 0;
+  return NMP_OK;
 }
 #endif
 

@@ -8,6 +8,7 @@ of one column set.
 from __future__ import annotations
 
 import ctypes as C
+import os
 from dataclasses import dataclass
 
 import numpy as np
@@ -153,6 +154,15 @@ class Engine:
                 if t is not None:
                     assert t.shape == (n,) and t.dtype == dt_ and t.is_contiguous()
                     assert t.device.type == "cuda" and t.device.index == self.device
+            if order is not None and os.environ.get("NMP_CHECK_ORDER") == "1":
+                # nmp_step_binned trusts order to be a permutation (noahmp_engine.h);
+                # the debug check costs a sort and a host sync per launch
+                with torch.cuda.stream(s):
+                    srt = torch.sort(order[lo:hi])[0]
+                    ok = bool(torch.equal(srt, torch.arange(hi - lo, dtype=torch.int32,
+                                                            device=order.device)))
+                if not ok:
+                    raise ValueError(f"order[{lo}:{hi}] is not a permutation of 0..{hi - lo - 1}")
             _lib.check(self._lib.nmp_step_binned(
                 self._h, hi - lo, n, zs, float(dt), float(julian), int(yearlen),
                 _ptr(cs.state, lo), _ptr(cs.isnow, lo), _ptr(cs.static_f, lo),

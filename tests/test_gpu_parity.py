@@ -19,6 +19,8 @@ libnoahmp_engine.so).  Two tiers:
 fp64 engine vs the fp64 restatement: |d| <= 1e-9 (1 + |ref|) on >= 99 % of
 columns (ocml vs glibc double libm ulps).
 """
+import dataclasses
+
 import numpy as np
 import pytest
 import torch
@@ -397,6 +399,31 @@ def test_rebinned_steps_equal_plain_steps(engines, tile, every):
         assert (o != np.arange(hi - lo)).any()
 
 
+def test_step_binned_order_check(engines, monkeypatch):
+    """nmp_step_binned trusts `order` (noahmp_engine.h precondition);
+    NMP_CHECK_ORDER=1 makes Engine.step refuse a non-permutation before any
+    launch, and pass a real one."""
+    from noahmp_amd.engine import ColumnState
+    from noahmp_amd.params import Params
+    n = 1000
+    eng = engines([L.CASE_NML_OPTIONS[k] for k in L.OPTION_NAMES])
+    cols = cases.make_columns(n, "mixed", Params.builtin().as_dict(), seed=3, julian=200.0)
+    F = torch.as_tensor(cases.forcing_step(cols, 200.0, 365, 0, seed=3), device=DEV)
+    cs = ColumnState.from_host(cols, DEV)
+    before = cs.state.clone()
+    monkeypatch.setenv("NMP_CHECK_ORDER", "1")
+    bad = torch.arange(n, dtype=torch.int32, device=DEV)
+    bad[5] = 4  # duplicate
+    for o in (bad, torch.full((n,), n, dtype=torch.int32, device=DEV)):
+        with pytest.raises(ValueError, match="not a permutation"):
+            eng.step(cs, F, cases.CASE_NML_ZSOIL, 1800.0, 200.0, 365, order=o)
+    torch.cuda.synchronize()
+    assert torch.equal(cs.state.view(torch.int32), before.view(torch.int32))
+    good = torch.flip(torch.arange(n, dtype=torch.int32, device=DEV), (0,))
+    eng.step(cs, F, cases.CASE_NML_ZSOIL, 1800.0, 200.0, 365, order=good)
+    torch.cuda.synchronize()
+
+
 @pytest.mark.parametrize("opt_veg,precision", [(1, 4), (2, 4), (1, 8), (2, 8)])
 def test_option_set_kernels_equal_generic(opt_veg, precision):
     """The compiled option-set kernels (case.nml options = set 1, + opt_veg 2
@@ -738,3 +765,87 @@ def test_year_trajectory_bit_exact_vs_oracle(engines, oracle_port, kind, opt_veg
         assert bad[pools][:, np.isin(vt, (26, 27))].all()
         bad[np.ix_(pools, np.isin(vt, (26, 27)))] = False
     assert not bad.any()
+
+
+def _redo_count(reset=True):
+    import ctypes as C
+    from noahmp_amd import lib as _l
+    v = C.c_ulonglong(0)
+    assert _l.load().nmp_div_redo_count(C.byref(v), int(reset)) == 0
+    return int(v.value)
+
+
+@pytest.mark.parametrize("fwet,variant", [(1e-30, "casenml"), (1e-7, "casenml"),
+                                          (1e-30, "generic"), (1e-30, "crs2"),
+                                          (1e-30, "veg2")])
+def test_fast_division_rerun_is_bit_exact(engines, oracle_port, fwet, variant):
+    """The canopy Newton loop divides through DivFast32 (csrc/sflx_math.h): a
+    shared, correctly rounded reciprocal and one residual correction, exact
+    while every operand stays in the guarded range.  Columns pushed outside it
+    -- a canopy wet fraction of 1e-30 or 1e-7, so that the loop-invariant
+    numerator FWET*VAIE fails d.chk's [2^-20, 2^20] -- must re-run the loop with the
+    reference's divisions (nmp_div_redo_count counts them) and still match the
+    C restatement bit for bit, as every untouched column does.  Variants: the
+    case.nml option-set kernel, the run-time-options kernel (option set 0
+    forced), Jarvis canopy resistance (opt_crs 2, set 0) and opt_veg 2 (set 2)."""
+    from noahmp_amd.engine import ColumnState, Engine
+    from noahmp_amd.params import Params
+    P = Params.builtin()
+    o = dict(L.CASE_NML_OPTIONS)
+    if variant == "crs2":
+        o["opt_crs"] = 2
+    if variant == "veg2":
+        o["opt_veg"] = 2
+    opts = [o[k] for k in L.OPTION_NAMES]
+    if variant == "generic":
+        eng = Engine(P, o, device=0, precision=4)
+        assert eng.option_set(0) == 0
+    else:
+        eng = engines(opts)
+    n = 4096
+    cols = cases.make_columns(n, "mixed", P.as_dict(), seed=21, julian=180.0)
+    st = cols.state.copy()
+    hit = np.arange(n) % 3 == 0
+    st[L.s("FWET").start, hit] = np.float32(fwet)
+    cols = dataclasses.replace(cols, state=st)
+    f = cases.forcing_step(cols, 180.3, 366, 0, seed=21)
+    cs = ColumnState.from_host(cols, DEV)
+    diag = torch.zeros((L.NDIAG_FULL, n), device=DEV)
+    _redo_count(reset=True)
+    eng.step(cs, torch.as_tensor(f, device=DEV), cases.CASE_NML_ZSOIL, 1800.0, 180.3, 366, diag,
+             L.DIAG_FULL_LEVEL)
+    torch.cuda.synchronize()
+    redo = _redo_count(reset=True)
+    est, eisn, edg, estat = oracle_port.step(load_params(), tuple(opts), cases.CASE_NML_ZSOIL, 1800.0,
+                                             366, 180.3, st, cols.isnow, cols.static_f,
+                                             cols.static_i, f)
+    got, gd = cs.state.cpu().numpy(), diag.cpu().numpy()
+    ok = bit_equal(got, est).all(0) & bit_equal(gd, edg).all(0)
+    assert ok.all(), f"{(~ok).sum()} columns differ ({int((~ok & hit).sum())} of them pushed)"
+    assert np.array_equal(cs.isnow.cpu().numpy(), eisn)
+    veg = edg[L.DIAG_FULL.index("FVEG")] > 0
+    print(variant, fwet, "option set", eng.option_set(), "re-runs", redo, "of",
+          int((hit & veg).sum()), "pushed vegetated columns")
+    assert redo >= 1
+    assert redo <= n
+
+
+def test_fast_division_rarely_reruns(engines):
+    """On the bench's own column set the guard almost never fails: the re-run
+    count over 2 steps of 262,144 mixed columns is below 0.1 % of the
+    vegetated column-steps (it is reported)."""
+    from noahmp_amd.engine import ColumnState
+    from noahmp_amd.params import Params
+    P = Params.builtin()
+    eng = engines([L.CASE_NML_OPTIONS[k] for k in L.OPTION_NAMES])
+    n = 262_144
+    cols = cases.make_columns(n, "mixed", P.as_dict(), seed=1000, julian=180.0)
+    cs = ColumnState.from_host(cols, DEV)
+    _redo_count(reset=True)
+    for s in range(2):
+        f = torch.as_tensor(cases.forcing_step(cols, 180.0 + s / 48, 366, s, seed=1000), device=DEV)
+        eng.step(cs, f, cases.CASE_NML_ZSOIL, 1800.0, 180.0 + s / 48, 366)
+    torch.cuda.synchronize()
+    redo = _redo_count(reset=True)
+    print("re-runs", redo, "of", 2 * n, "column-steps")
+    assert redo <= 2 * n // 1000

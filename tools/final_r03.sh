@@ -27,6 +27,10 @@ timeout -k 10 400 python bench.py > "$OUT/bench.log" 2>&1
 rc=$?; echo "bench rc=$rc"; tail -1 "$OUT/bench.log"; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 python bench.py --steps 20 --warmup 5 --no-cpu-baseline > "$OUT/bench_driver_args.log" 2>&1
 rc=$?; echo "bench (driver args) rc=$rc"; tail -1 "$OUT/bench_driver_args.log"; [ $rc -eq 0 ] || exit $rc
+# same build, the generator's shuffled column order: the speedup due to the
+# coherent order alone (the headline uses --order lon-snow-type)
+timeout -k 10 300 python bench.py --order as-generated --no-cpu-baseline > "$OUT/bench_as_generated.log" 2>&1
+rc=$?; echo "bench (as-generated order) rc=$rc"; tail -1 "$OUT/bench_as_generated.log"; [ $rc -eq 0 ] || exit $rc
 if [ "${SKIP_DIST:-0}" != 1 ]; then
   timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29531 bench.py --gpus 1 --no-cpu-baseline > "$OUT/bench_dist_n1.log" 2>&1
   rc=$?; echo "torchrun bench rc=$rc"; tail -1 "$OUT/bench_dist_n1.log"; [ $rc -eq 0 ] || exit $rc
