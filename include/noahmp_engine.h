@@ -391,12 +391,6 @@ int nmp_set_cols_per_wave(nmp_engine* eng, int cpw);
 int nmp_option_set(nmp_engine* eng, int request);
 
 int nmp_engine_info(const nmp_engine* eng, int* device, int* precision, nmp_options* opts);
-/* Diagnostic (no reference counterpart): how many column-steps of the fp32
- * "ref" kernels re-ran the canopy Newton loop with the reference's IEEE
- * divisions because an operand left the range where the loop's faster
- * division is exact (DESIGN.md "Division in the canopy loop"); *out receives
- * the count since the last reset, reset != 0 clears it.  Process-wide. */
-int nmp_div_redo_count(unsigned long long* out, int reset);
 void nmp_finalize(nmp_engine* eng);
 const char* nmp_strerror(int code);
 int nmp_abi_version(void);

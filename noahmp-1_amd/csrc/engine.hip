@@ -19,18 +19,7 @@
 
 #include "sflx_kargs.h"
 
-// The fp32 kernels' fast-division fallback queue (sflx_kernel.hip
-// sflx_redo_kernel) of one stream: launches on one stream run in order and the
-// fallback kernel clears its queue at its end, so one queue per stream serves
-// every launch on it.  cap = queued waves it holds (grown on demand).
-struct RedoQueue {
-  hipStream_t stream;
-  uint32_t* buf;
-  int64_t cap;
-};
-
 struct nmp_engine {
-  std::vector<RedoQueue> redo;
   int device;
   int precision;
   int math;  // 0 = reference-rounded transcendentals (parity), 1 = fast (fp32 only)
@@ -117,32 +106,6 @@ void fill_args(nmp::KArgs<T>& a, const nmp_engine* e, int64_t ncol, int64_t ld,
   a.cpw = cols_per_wave(e, ncol);
 }
 
-// the stream's fallback queue with room for `waves` entries (see RedoQueue)
-uint32_t* redo_queue(nmp_engine* e, hipStream_t stream, int64_t waves) {
-  RedoQueue* q = nullptr;
-  for (auto& r : e->redo)
-    if (r.stream == stream) q = &r;
-  if (q && q->cap >= waves) return q->buf;
-  const int64_t cap = waves < 4096 ? 4096 : waves;
-  uint32_t* buf = nullptr;
-  if (hipMalloc(&buf, (size_t)(2 + cap) * sizeof(uint32_t)) != hipSuccess) return nullptr;
-  if (hipMemsetAsync(buf, 0, 2 * sizeof(uint32_t), stream) != hipSuccess) {
-    hipFree(buf);
-    return nullptr;
-  }
-  if (q) {
-    // a bigger launch on this stream: the old queue may still be in use by
-    // its last fallback launch
-    if (hipStreamSynchronize(stream) != hipSuccess) return nullptr;
-    hipFree(q->buf);
-    q->buf = buf;
-    q->cap = cap;
-  } else {
-    e->redo.push_back(RedoQueue{stream, buf, cap});
-  }
-  return buf;
-}
-
 int launch(nmp_engine* e, int64_t ncol, int64_t ld, const float zsoil[4], float dt,
            float julian, int32_t yearlen, void* state, int32_t* isnow, const void* sf,
            const int32_t* si, const void* fc, void* diag, int diag_level, int32_t* status,
@@ -154,18 +117,12 @@ int launch(nmp_engine* e, int64_t ncol, int64_t ld, const float zsoil[4], float 
     fill_args(a, e, ncol, ld, zsoil, dt, julian, yearlen, state, isnow, sf, si, fc, diag,
               diag_level, status, order, cost, ficeold);
     const bool small = small_launch(e, ncol);
-    a.redo = nullptr;
-    if (e->math == 0 && ncol > 0) {
-      a.redo = redo_queue(e, stream, (ncol + a.cpw - 1) / a.cpw);
-      if (!a.redo) return NMP_E_DEVICE;
-    }
     err = (e->math == 0) ? nmp::launch_sflx<float, true>(e->dparams, a, stream, small, e->os)
                          : nmp::launch_sflx<float, false>(e->dparams, a, stream, small, 0);
   } else {
     nmp::KArgs<double> a;
     fill_args(a, e, ncol, ld, zsoil, dt, julian, yearlen, state, isnow, sf, si, fc, diag,
               diag_level, status, order, cost, ficeold);
-    a.redo = nullptr;
     err = nmp::launch_sflx<double, false>(e->dparams, a, stream, small_launch(e, ncol), e->os);
   }
   return err == hipSuccess ? NMP_OK : NMP_E_DEVICE;
@@ -680,7 +637,6 @@ void nmp_finalize(nmp_engine* eng) {
   if (!eng) return;
   ensure_device(eng->device);
   if (eng->dparams) hipFree(eng->dparams);
-  for (auto& q : eng->redo) hipFree(q.buf);
   delete eng;
 }
 

@@ -47,10 +47,6 @@ struct KArgs {
   // columns stepped per 64-lane wave (8..64, a multiple of 8): below 64 the
   // launch spreads a small column set over more waves (small-N latency hiding)
   int cpw;
-  // the fp32 "ref" kernels' fast-division fallback queue of this launch's
-  // stream (engine.hip RedoQueue): [0] count, [1] finished workgroups of the
-  // fallback kernel, [2..] first launch index of each queued wave
-  uint32_t* redo;
 };
 
 template <class T, bool R>

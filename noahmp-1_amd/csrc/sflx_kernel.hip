@@ -802,10 +802,6 @@ DEV void gst(T* p, T v) {
   else *p = v;
 }
 
-// lanes of all launches that re-ran the canopy loop with the reference's
-// divisions (DivFast32 guard failed); read and reset by nmp_div_redo_count
-static __device__ unsigned long long nmp_div_redo;
-
 template <class T>
 struct Sink {
   T* dg;        // diag + column (NULL when level == NMP_DIAG_NONE)
@@ -845,9 +841,6 @@ struct Sink {
   }
   DEV void s(int f, T v) const { gst(st + f * ld, v); }
   DEV void isn(int v) const { gst(isnow, (int32_t)v); }
-  // a lane that re-ran the canopy Newton loop with the reference's divisions
-  // (the fast division's guard failed; nmp_engine_info's counter, tests)
-  static DEV void count_redo() { atomicAdd(&nmp_div_redo, 1ull); }
   // re-binning key: the vege_flux Newton trip count of this step (0 = no canopy)
   DEV void trips(int n) const {
     if (cost) *cost = (uint8_t)n;
@@ -937,14 +930,6 @@ static __device__ unsigned long long nmp_wave_rec[4 * NMP_WAVE_REC_MAX];
 static __device__ unsigned int nmp_wave_ctr;
 #endif
 
-// The canopy Newton loop's fp32 divisions through DivFast32 (sflx_math.h):
-// the "ref" fp32 kernels; NMP_FAST_DIV=0 keeps the reference's IEEE sequence
-// (A/B only, results identical).
-#ifndef NMP_FAST_DIV
-#define NMP_FAST_DIV 1
-#endif
-template <class T, bool R>
-constexpr bool kFastDiv = NMP_FAST_DIV != 0 && sizeof(T) == 4 && R;
 
 // Unroll factor of the vege_flux Newton loop (tuning knob, results identical).
 #ifndef NMP_VEGE_UNROLL
@@ -973,15 +958,9 @@ constexpr Opt kOptionSet[3] = {{1, 1, 1, 1, 1, 1, 1, 1, 2, 1, 1, 1},
                                {1, 1, 1, 1, 1, 1, 1, 1, 2, 1, 1, 1},
                                {2, 1, 1, 1, 1, 1, 1, 1, 2, 1, 1, 1}};
 
-// FD: the canopy Newton loop divides with DivFast32 (sflx_math.h) where the
-// policy allows it (kFastDiv).  Such a call returns false -- with nothing
-// stored that the column's re-run reads -- when any canopy lane of the wave
-// left the fast division's exact range; the caller then steps the wave's
-// columns again with FD = false (column_ref).  Otherwise it returns true.
-template <class T, bool R, int OS, bool FD>
-DEV bool sflx_column(const DevParams& P, const KArgs<T>& A, Col<T>& c, const Sink<T>& out) {
+template <class T, bool R, int OS>
+DEV void sflx_column(const DevParams& P, const KArgs<T>& A, Col<T>& c, const Sink<T>& out) {
   typedef Mth<T, R> M;
-  constexpr bool kFD = FD && kFastDiv<T, R>;
 
 #ifdef NMP_PHASE_TIMING
   PhaseClock pclk{__builtin_amdgcn_s_memtime(), 0};
@@ -1216,10 +1195,8 @@ DEV bool sflx_column(const DevParams& P, const KArgs<T>& A, Col<T>& c, const Sin
     fsun = (L(1.0) - M::exp(-ext * vaia)) / rmax(ext * vaia, mpe6);
     ext = fsun;
     fsun = (ext < L(0.01)) ? L(0.) : ext;
-    if constexpr (!kFD) {
-      out.s(NMP_S_ALBOLD, c.albold);
-      out.s(NMP_S_TAUSS, c.tauss);
-    }
+    out.s(NMP_S_ALBOLD, c.albold);
+    out.s(NMP_S_TAUSS, c.tauss);
   }
   T fsha = L(1.0) - fsun;
   T laisun = elai * fsun;
@@ -1333,7 +1310,6 @@ DEV bool sflx_column(const DevParams& P, const KArgs<T>& A, Col<T>& c, const Sin
   // ---- vege_flux: func.f90:2465-2964 ----
   T tgv = L(0.0), cmv = L(0.0);
   int vtrips = 0;
-  bool need_ref = false;  // this lane's canopy loop left DivFast32's range
   if (veg && fveg > L(0.0)) {
     tgv = c.tg;
     const T mpe = L(1E-6);
@@ -1465,15 +1441,8 @@ DEV bool sflx_column(const DevParams& P, const KArgs<T>& A, Col<T>& c, const Sin
         if (iter >= 5 && fabs(dtv) <= L(0.01) && liter == 0) liter = 1;
       }
     };
-    if constexpr (kFD) {
-      DivFast32 df;
-      vege_loop(df);
-      // (probes: NMP_FAST_DIV 2 = never re-run (timing), 3 = always)
-      need_ref = NMP_FAST_DIV == 3 || (NMP_FAST_DIV != 2 && !df.ok());
-    } else {
-      DivRef<T> dr;
-      vege_loop(dr);
-    }
+    DivRef<T> dr;
+    vege_loop(dr);
     // under-canopy fluxes and TG (loop2, :2881-2914)
     air = -emg * (L(1.0) - emv) * c.lwdn - emg * emv * SB * p4(c.tv);
     cir = emg * SB;
@@ -1518,16 +1487,6 @@ NMP_UNROLL(NMP_LOOP2_UNROLL)
     chv = cah;
     chleaf = cvh;
     chuc = L(1.0) / rahg;
-  }
-  if constexpr (kFD) {
-    // every lane of the wave is active again here: a wave-uniform decision.
-    // Nothing the re-run reads has been stored yet (the diagnostics written so
-    // far are rewritten with the same values; ALBOLD/TAUSS were held back).
-    if (__builtin_amdgcn_ballot_w64(need_ref) != 0) return false;
-    if (c.cosz > L(0.0)) {
-      out.s(NMP_S_ALBOLD, c.albold);
-      out.s(NMP_S_TAUSS, c.tauss);
-    }
   }
   out.trips(vtrips);
 
@@ -1995,7 +1954,7 @@ NMP_UNROLL(kBareUnroll)
   out.template d<NMP_D_EDIR>(edir);
   out.s(NMP_S_SNEQVO, c.sneqvo);
 #ifdef NMP_TRUNC_ENERGY
-  return true;  // timing experiment only (tools/build_variants.py): the energy phase alone
+  return;  // timing experiment only (tools/build_variants.py): the energy phase alone
 #endif
 
   NMP_PHASE(9);
@@ -2810,7 +2769,6 @@ NMP_UNROLL(kBareUnroll)
   out.template d<NMP_D_Q2B>(q2b);
   out.s(NMP_S_QSFC, c.qsfc); out.s(NMP_S_SNOWH, c.snowh); out.s(NMP_S_SNEQV, c.sneqv);
   NMP_PHASE(15);
-  return true;
 }
 
 // ---------------------------------------------------------------------------
@@ -2944,19 +2902,8 @@ void sflx_step_kernel(const DevParams* __restrict__ gparams,
   // copy is issued first; the column's other fields load while it is in flight
   if constexpr (kPrefetch<T, R>) copy_layers_to_lds(st0, a.ld);
   NMP_LOAD_COLUMN(T, R);
-  if (sflx_column<T, R, OS, true>(sp, a, c, out)) {
-    if (c.status != 0) a.status[c0] |= c.status;
-  } else {
-    // (kFastDiv kernels only) a canopy lane of this wave left the fast
-    // division's range: nothing is stored that a re-run reads, so the wave is
-    // queued whole for sflx_redo_kernel, launched right after this one.  One
-    // lane appends the wave's first launch index.
-    const uint64_t live = __builtin_amdgcn_read_exec();
-    if (lane == __builtin_ctzll(live)) {
-      const uint32_t i = atomicAdd(a.redo, 1u);
-      a.redo[2 + i] = (uint32_t)(gid - lane);
-    }
-  }
+  sflx_column<T, R, OS>(sp, a, c, out);
+  if (c.status != 0) a.status[c0] |= c.status;
 #ifdef NMP_WAVE_TIMING
   {
     const unsigned long long wt1 = __builtin_amdgcn_s_memrealtime();
@@ -2977,52 +2924,6 @@ void sflx_step_kernel(const DevParams* __restrict__ gparams,
 #endif
 }
 
-// The fast-division fallback: the waves the step kernel queued in a.redo
-// (redo[0] = count, redo[1] = finished workgroups, redo[2..] = each wave's
-// first launch index) stepped again with the reference's divisions.  A
-// separate kernel, because the re-run code inside the step kernel -- inlined
-// or as a call -- costs the step kernel registers on every launch (inlined:
-// 36 -> 110 spilled VGPRs; a call: 36 -> 148, and 7 % of the step).  A small
-// fixed grid; with nothing queued every workgroup returns at once.  The last
-// workgroup to finish clears the queue for the stream's next launch.
-template <class T, bool R, int OS>
-__global__ __launch_bounds__(NMP_BLOCK)
-__attribute__((amdgpu_waves_per_eu(waves_per_eu<T>(false))))
-void sflx_redo_kernel(const DevParams* __restrict__ gparams, KArgs<T> a) {
-  const uint32_t n = __hip_atomic_load(a.redo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  if (n == 0) return;
-  __shared__ __attribute__((aligned(16))) DevParams sp;
-  {
-    const int4* src = reinterpret_cast<const int4*>(gparams);
-    int4* dst = reinterpret_cast<int4*>(&sp);
-    constexpr int NW = sizeof(DevParams) / sizeof(int4);
-    for (int i = threadIdx.x; i < NW; i += blockDim.x) dst[i] = src[i];
-  }
-  if constexpr (sizeof(T) == 4 && R) stage_math_tables();
-  __syncthreads();
-  const int lane = threadIdx.x & 63;
-  const uint32_t stride = gridDim.x * (NMP_BLOCK / 64);
-  for (uint32_t j = blockIdx.x * (NMP_BLOCK / 64) + (threadIdx.x >> 6); j < n; j += stride) {
-    const int64_t gid = (int64_t)a.redo[2 + j] + lane;
-    if (lane < a.cpw && gid < a.ncol) {
-      const int64_t c0 = a.order ? (int64_t)a.order[gid] : gid;
-      if constexpr (kPrefetch<T, R>) copy_layers_to_lds(a.state + c0, a.ld);
-      NMP_LOAD_COLUMN(T, R);
-      sflx_column<T, R, OS, false>(sp, a, c, out);
-      if (c.status != 0) a.status[c0] |= c.status;
-      Sink<T>::count_redo();
-    }
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    __threadfence();
-    if (atomicAdd(a.redo + 1, 1u) == gridDim.x - 1) {
-      a.redo[0] = 0u;
-      a.redo[1] = 0u;
-    }
-  }
-}
-
 // launch wrapper (one instantiation per precision / math policy)
 template <class T, bool R, bool SMALL>
 void launch_os(int os, dim3 grid, dim3 block, hipStream_t stream, const DevParams* dparams,
@@ -3033,19 +2934,6 @@ void launch_os(int os, dim3 grid, dim3 block, hipStream_t stream, const DevParam
     hipLaunchKernelGGL((sflx_step_kernel<T, R, SMALL, 2>), grid, block, 0, stream, dparams, a);
   else
     hipLaunchKernelGGL((sflx_step_kernel<T, R, SMALL, 0>), grid, block, 0, stream, dparams, a);
-}
-
-// the fast-division fallback after a step launch (kFastDiv kernels only):
-// one workgroup per 16 CUs' worth of waves -- the queue is normally empty
-template <class T, bool R>
-void launch_redo(int os, hipStream_t stream, const DevParams* dparams, const KArgs<T>& a) {
-  const dim3 grid(64), block(NMP_BLOCK);
-  if (os == 1)
-    hipLaunchKernelGGL((sflx_redo_kernel<T, R, 1>), grid, block, 0, stream, dparams, a);
-  else if (os == 2)
-    hipLaunchKernelGGL((sflx_redo_kernel<T, R, 2>), grid, block, 0, stream, dparams, a);
-  else
-    hipLaunchKernelGGL((sflx_redo_kernel<T, R, 0>), grid, block, 0, stream, dparams, a);
 }
 
 // launch wrapper (one instantiation per precision / math policy).  os: the
@@ -3059,12 +2947,10 @@ hipError_t launch_sflx(const DevParams* dparams, const KArgs<T>& a, hipStream_t 
   if (grid == 0) return hipSuccess;
   // the fast-math fp32 path has neither a small nor option-set instantiation (code size)
   if constexpr (sizeof(T) == 8 || R) {
-    if (kFastDiv<T, R> && !a.redo) return hipErrorInvalidValue;  // the fallback queue
     if (small)
       launch_os<T, R, true>(os, dim3((unsigned)grid), dim3(block), stream, dparams, a);
     else
       launch_os<T, R, false>(os, dim3((unsigned)grid), dim3(block), stream, dparams, a);
-    if constexpr (kFastDiv<T, R>) launch_redo<T, R>(os, stream, dparams, a);
   } else {
     hipLaunchKernelGGL((sflx_step_kernel<T, R, false, 0>), dim3((unsigned)grid), dim3(block), 0,
                        stream, dparams, a);
@@ -3107,21 +2993,6 @@ extern "C" int nmp_debug_phase_cycles(unsigned long long* out16, int reset) {
 #endif
 
 
-#if !defined(NMP_TU) || NMP_TU == 4
-// the canopy-loop re-runs of the fp32 kernels (DivFast32's guard): the count
-// since the last reset; reset != 0 clears it afterwards
-extern "C" int nmp_div_redo_count(unsigned long long* out, int reset) {
-  if (!out) return NMP_E_ARG;
-  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(nmp_div_redo), sizeof(*out)) != hipSuccess)
-    return NMP_E_DEVICE;
-  if (reset) {
-    const unsigned long long z = 0;
-    if (hipMemcpyToSymbol(HIP_SYMBOL(nmp_div_redo), &z, sizeof(z)) != hipSuccess)
-      return NMP_E_DEVICE;
-  }
-  return NMP_OK;
-}
-#endif
 
 #if defined(NMP_WAVE_TIMING) && (!defined(NMP_TU) || NMP_TU == 4)
 // the fp32 kernels' wave records: copies min(count, max_rec) records of 4 u64

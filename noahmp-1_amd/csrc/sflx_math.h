@@ -207,27 +207,11 @@ __device__ __forceinline__ double dv<double>(double a, double b) {
 // div_scale / div_fmas / div_fixup sequence, 11 instructions and a vcc chain
 // per division), `dv` in fp64.
 //
-// DivFast32 (fp32, bit-identical to DivRef wherever its guard holds): the
-// reciprocal r = fma(fma(-b, r0, 1), r0, r0) from v_rcp_f32, then q = a*r, one
-// fma residual correction and v_div_fixup_f32 (zeros, infinities, NaNs).
-// Checked on the GPU itself (tools/fdiv_exhaust.hip, profiles/r03/fdiv_exhaust2.txt):
-// r equals the correctly rounded 1/b for every normal b with a normal 1/b
-// (2^32 patterns), r scales exactly with b's exponent, and the quotient
-// equals IEEE a/b for every pair of significands (2^46 pairs) -- so for every
-// a, b whose intermediates stay normal; 10^9 random pairs with |a| in
-// {0} U [2^-60, 2^60] and |b| in [2^-60, 2^60] agree, outside that range ~1 %
-// do not.  The guard records, per lane, the ranges that make it exact:
-//   hi = max(|b|, |r|, |q|)   <= 2^60: every denominator in [2^-60, 2^60], no
-//                             quotient (hence no numerator) near overflow;
-//   lo = min((bits(q) << 1) - 1) >= bits of 2^-40: every quotient of div() is 0
-//                             or >= 2^-40, so its numerator is 0 or >= 2^-100
-//                             (the fma residual stays exact);
-//   chk(a) for divk numerators: 0 or |a| in [2^-20, 2^20].
-// A zero, infinite or NaN operand is handled by v_div_fixup exactly as in the
-// IEEE sequence (a zero or infinite denominator trips hi).  A lane whose guard
-// fails re-runs the whole loop with DivRef (sflx_column), so every lane's
-// results are the reference's bits; the guard almost never fails on physical
-// data (tests count the re-runs).
+// A faster fp32 policy (a shared v_rcp_f32 reciprocal, one fma residual
+// correction and v_div_fixup, exact while a per-lane range guard holds, with a
+// wave re-run through DivRef when it does not) was built and measured in round
+// 3 and removed: no faster than the IEEE sequence once guarded, and one build
+// of it stepped columns wrong (DESIGN.md "Division in the canopy loop").
 template <class T>
 struct Recip {
   T b, r;
@@ -239,73 +223,6 @@ struct DivRef {
   __device__ __forceinline__ T div(T a, const Recip<T>& R) const { return dv(a, R.b); }
   __device__ __forceinline__ T divk(T a, const Recip<T>& R) const { return dv(a, R.b); }
   __device__ __forceinline__ void chk(T) const {}
-  __device__ __forceinline__ bool ok() const { return true; }
-};
-
-#ifndef NMP_DIV_GUARD
-#define NMP_DIV_GUARD 0
-#endif
-struct DivFast32 {
-#if NMP_DIV_GUARD == 2
-  // (probe) one accumulator: the largest |binary exponent| of every
-  // denominator and quotient (frexp; zero, infinity and NaN count as 0)
-  int m = 0;
-  __device__ __forceinline__ void track(float x) {
-    const int e = __builtin_amdgcn_frexp_expf(x);
-    m = max(m, max(e, -e));
-  }
-#else
-  float hi = 0.0f;
-  uint32_t lo = 0xffffffffu;
-#endif
-  __device__ __forceinline__ Recip<float> rec(float b) {
-    float r = __builtin_amdgcn_rcpf(b);
-    const float e = __builtin_fmaf(-b, r, 1.0f);
-    r = __builtin_fmaf(e, r, r);
-#if NMP_DIV_GUARD == 2
-    track(b);
-#elif NMP_DIV_GUARD == 1
-    hi = __builtin_fmaxf(hi, __builtin_fabsf(b));
-    const uint32_t y = __float_as_uint(b) << 1;  // (0 fails here)
-    lo = y < lo ? y : lo;
-#else
-    hi = __builtin_fmaxf(hi, __builtin_fmaxf(__builtin_fabsf(b), __builtin_fabsf(r)));
-#endif
-    return {b, r};
-  }
-  __device__ __forceinline__ float divk(float a, const Recip<float>& R) const {
-    float q = a * R.r;
-    const float e = __builtin_fmaf(-R.b, q, a);
-    q = __builtin_fmaf(e, R.r, q);
-    return __builtin_amdgcn_div_fixupf(q, R.b, a);
-  }
-  __device__ __forceinline__ float div(float a, const Recip<float>& R) {
-    const float q = divk(a, R);
-#if NMP_DIV_GUARD == 2
-    track(q);
-#else
-    hi = __builtin_fmaxf(hi, __builtin_fabsf(q));
-    const uint32_t y = (__float_as_uint(q) << 1) - 1u;
-    lo = y < lo ? y : lo;
-#endif
-    return q;
-  }
-  __device__ __forceinline__ void chk(float a) {
-    // 0 or |a| in [2^-20, 2^20]: scaled into the hi / lo windows above
-#if NMP_DIV_GUARD == 2
-    if (a != 0.0f && !(__builtin_fabsf(a) >= 0x1p-20f && __builtin_fabsf(a) <= 0x1p20f)) m = 999;
-#else
-    hi = __builtin_fmaxf(hi, __builtin_fabsf(a) * 0x1p40f);
-    if (a != 0.0f && __builtin_fabsf(a) < 0x1p-20f) lo = 0u;
-#endif
-  }
-  __device__ __forceinline__ bool ok() const {
-#if NMP_DIV_GUARD == 2
-    return m <= 40;
-#else
-    return hi <= 0x1p60f && lo >= ((uint32_t)(127 - 40) << 24) - 1u;
-#endif
-  }
 };
 
 // Register-array access with a runtime index, lowered to a select chain so the

@@ -38,9 +38,13 @@ def oracle_port():
 
 @pytest.fixture(scope="session")
 def engine_lib():
-    """The engine C-ABI library (built on demand with hipcc, no fallback)."""
+    """The engine C-ABI library (built on demand with hipcc, no fallback).  A
+    tuning variant named by NOAHMP_ENGINE_LIB (tools/build_variants.py) is
+    loaded as built: rebuilding it here would replace it with the default
+    build's flags."""
     from noahmp_amd import build, lib
-    build.build()
+    if build.LIB_PATH == build.DEFAULT_LIB_PATH:
+        build.build()
     return lib.load()
 
 

@@ -71,11 +71,6 @@ VARIANTS = {
     "nocrdiv": ("-fno-hip-fp32-correctly-rounded-divide-sqrt",),
     "fdiv9": {"f32": ["-DNMP_F32_DIV=9"]},
     "cr9": {"f32": ["-DNMP_F32_DIV=1"]},
-    "fd0": {"f32": ["-DNMP_FAST_DIV=0"]},
-    "fd2": {"f32": ["-DNMP_FAST_DIV=2"]},
-    "fd3": {"f32": ["-DNMP_FAST_DIV=3"]},
-    "g1": {"f32": ["-DNMP_DIV_GUARD=1"]},
-    "g2": {"f32": ["-DNMP_DIV_GUARD=2"]},
     "ldswait0": {"f32": ["-DNMP_LDS_EXPLICIT_WAIT=0"]},
     "fdiv7": {"f32": ["-DNMP_F32_DIV=7"]},
     "nopeel": ("-DNMP_VEGE_NOPEEL",),
