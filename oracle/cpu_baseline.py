@@ -112,11 +112,15 @@ def cpu_model() -> str:
 
 
 def _worker(args):
-    i, cpu, kind, cols_per, nsteps, t_start, precision = args
+    i, nw, cpu, kind, cols_per, nsteps, t_start, precision = args
     from noahmp_amd import cases  # package registered by the parent
     os.sched_setaffinity(0, {cpu})
     c = _CTX
-    cols = c["cols"].take(np.arange(i * cols_per, (i + 1) * cols_per))
+    # every nw-th column from i: each worker's sample spans the whole column
+    # set (the bench's set is in coherent order -- latitude bands, snow,
+    # vegetation type -- so contiguous slices gave workers unequal work and
+    # the slowest set the wall)
+    cols = c["cols"].take(np.arange(i, nw * cols_per, nw))
     Fa = np.stack([cases.forcing_step(cols, c["julian0"] + s * c["dt"] / 86400.0, c["yearlen"], s,
                                       seed=c["seed"]) for s in range(min(nsteps, c["period"]))])
     if kind == "reference":
@@ -159,7 +163,8 @@ def measure(cols, params: dict, options: tuple, zsoil, dt: float, julian0: float
     def timed(kind, precision):
         t_start = time.time() + 2.0 + 0.02 * workers
         with mp.get_context("fork").Pool(workers) as pool:
-            el = pool.map(_worker, [(i, cpus[i], kind, cols_per_worker, nsteps, t_start, precision)
+            el = pool.map(_worker, [(i, workers, cpus[i], kind, cols_per_worker, nsteps, t_start,
+                                     precision)
                                     for i in range(workers)])
         return max(el)
 
@@ -171,8 +176,8 @@ def measure(cols, params: dict, options: tuple, zsoil, dt: float, julian0: float
         "C restatement -O2"
     out = {"value": value, "unit": "column-steps/s", "cores": workers, "kind": kind,
            "sample": (f"{workers} single-threaded processes, one per physical core (SMT siblings "
-                      f"idle), x {cols_per_worker} columns x {nsteps} steps of the bench column "
-                      f"set ({what}; time loop inside the library), wall {wall:.1f} s"),
+                      f"idle), x {cols_per_worker} columns (stride {workers} from the worker's "
+                      f"index) x {nsteps} steps of the bench column set ({what}; time loop inside the library), wall {wall:.1f} s"),
            "per_core": value / workers,
            "host_physical_cores": phys,
            "whole_host_estimate": value / workers * phys,
