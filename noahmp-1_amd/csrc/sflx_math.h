@@ -242,8 +242,19 @@ __device__ __forceinline__ T pin(T v) {
 template <class T, int N>
 __device__ __forceinline__ T dget(const T (&a)[N], int i) {
   T r = pin(a[0]);
+#ifdef NMP_DGET_BRANCHY
+  // (A/B only) the pin inside the select: the volatile asm cannot be
+  // speculated, so every element becomes an exec-masked branch
 #pragma unroll
   for (int k = 1; k < N; ++k) r = (i == k) ? pin(a[k]) : r;
+#else
+  // every element pinned unconditionally, then selected: one v_cndmask each
+#pragma unroll
+  for (int k = 1; k < N; ++k) {
+    const T v = pin(a[k]);
+    r = (i == k) ? v : r;
+  }
+#endif
   return r;
 }
 template <class T, int N>

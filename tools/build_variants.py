@@ -72,6 +72,7 @@ VARIANTS = {
     "fdiv9": {"f32": ["-DNMP_F32_DIV=9"]},
     "cr9": {"f32": ["-DNMP_F32_DIV=1"]},
     "ldswait0": {"f32": ["-DNMP_LDS_EXPLICIT_WAIT=0"]},
+    "dgetbr": ("-DNMP_DGET_BRANCHY",),
     "fdiv7": {"f32": ["-DNMP_F32_DIV=7"]},
     "nopeel": ("-DNMP_VEGE_NOPEEL",),
     "vu2": ("-DNMP_VEGE_UNROLL=2",),
