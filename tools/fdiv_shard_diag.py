@@ -1,7 +1,8 @@
 """Diagnostic (GPU box): the stream-shard scenario of
 tests/test_gpu_parity.py::test_stream_shards_equal_single_launch, step by
 step, for the library NOAHMP_ENGINE_LIB names (round 3: the guarded
-fast-division builds, since removed -- profiles/r03/fdiv_shard_diag_*.txt).  After each step the sharded
+fast-division builds of commit 5cd66f0 with -DNMP_FAST_DIV/-DNMP_DIV_GUARD
+variants, since removed -- profiles/r03/fdiv_shard_diag_*.txt).  After each step the sharded
 and single-launch states are compared; on the first difference both are
 compared with the C restatement (oracle, checker only) stepped from the same
 start state, and the differing columns are listed with their fields.
