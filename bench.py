@@ -303,7 +303,7 @@ def main():
         F = torch.empty((a.period, L.NFORCING, n), dtype=dtype, device=dev)
         for s in range(a.period):
             F[s].copy_(torch.from_numpy(cases.forcing_step(
-                cols, julian0 + s * a.dt / 86400.0, yearlen, s, seed=seed)))
+                cols, (julian0 + s * a.dt / 86400.0) % yearlen, yearlen, s, seed=seed)))
     else:
         # two forcing buffers: step k writes buffer k % 2 on each range's stream
         # right before that range's launch (stream order makes reuse safe)
@@ -334,7 +334,9 @@ def main():
         """Bench step k: every column range on its own stream (StreamShards), plus the
         async diagnostics gather on output steps (shard.OutputSchedule)."""
         d = sched.diag_for(k)
-        jul = julian0 + k * a.dt / 86400.0
+        # day of year: the calendar wraps at yearlen (a run past the year's end
+        # continues into the next year; the engine rejects julian > yearlen)
+        jul = (julian0 + k * a.dt / 86400.0) % yearlen
         if a.forcing == "resident":
             f, pre = F[k % a.period], None
         else:

@@ -245,7 +245,9 @@ int nmp_init(const nmp_params* params, const nmp_options* opts, int device, int 
 
 /* One noahmp_sflx time step for ncol columns (all pointers device, SoA with
  * leading dimension ld).  zsoil[4] (<0, m) and dt are domain-wide; julian /
- * yearlen are the step's calendar position (noahmp_sflx :67).  FICEOLD is
+ * yearlen are the step's calendar position (noahmp_sflx :67), 0 <= julian <=
+ * yearlen, else NMP_E_ARG (outside it the reference's phenology reads its
+ * monthly LAI/SAI tables out of bounds).  FICEOLD is
  * derived on device from SNICE/SNLIQ at step start, as an offline driver does.
  * diag may be NULL when diag_level == NMP_DIAG_NONE; col_status is OR-ed
  * (caller zeroes it when it wants a fresh mask). */
@@ -281,8 +283,9 @@ int nmp_rebin(nmp_engine* eng, int64_t ncol, const uint8_t* cost, int32_t* order
 /* Same step, many times: nsteps steps (one launch each, enqueued on stream)
  * whose forcing slices are forcing + (s % forcing_period)*forcing_stride
  * (elements, real type; forcing_period 0 = nsteps distinct slices), julian
- * advancing by dt/86400 per step (julian0 + (float)s*dt/86400.0f); bitwise the
- * same as nsteps nmp_step calls.  diag (if non-NULL) receives the last step only. */
+ * advancing by dt/86400 per step (julian0 + (float)s*dt/86400.0f, every one
+ * within [0, yearlen], else NMP_E_ARG: split a run at the year boundary);
+ * bitwise the same as nsteps nmp_step calls.  diag (if non-NULL) receives the last step only. */
 /* Synthetic forcing for one step, generated on the device (no reference
  * counterpart: the reference reads LDASIN files, run/case.nml:6-7, and ships
  * none).  Writes the 12 NMP_A_* fields of ncol columns

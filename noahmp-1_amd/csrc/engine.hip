@@ -128,6 +128,14 @@ int launch(nmp_engine* e, int64_t ncol, int64_t ld, const float zsoil[4], float 
   return err == hipSuccess ? NMP_OK : NMP_E_DEVICE;
 }
 
+// The calendar position noahmp_sflx accepts: 0 <= julian <= yearlen (NaN
+// fails).  Outside it the reference's phenology indexes its 12-month LAI/SAI
+// tables out of bounds (func.f90 phenology, IT1 = FLOOR(12*(DAY-0.5)/YEARLEN
+// + 0.5) > 12), so such a step has no defined result.
+bool julian_ok(float julian, int32_t yearlen) {
+  return julian >= 0.0f && julian <= (float)yearlen;
+}
+
 int check_common(const nmp_engine* eng, int64_t ncol, int64_t ld, const float zsoil[4], float dt,
                  int32_t yearlen, const void* state, const int32_t* isnow, const void* static_f,
                  const int32_t* static_i, const void* forcing, const void* diag, int diag_level,
@@ -241,6 +249,7 @@ int nmp_step(nmp_engine* eng, int64_t ncol, int64_t ld, const float zsoil[4], fl
              int32_t* col_status, void* stream) {
   if (!eng || ncol < 0) return NMP_E_ARG;
   if (ncol == 0) return NMP_OK;
+  if (!julian_ok(julian, yearlen)) return NMP_E_ARG;
   int rc = check_common(eng, ncol, ld, zsoil, dt, yearlen, state, isnow, static_f, static_i,
                         forcing, diag, diag_level, col_status);
   if (rc != NMP_OK) return rc;
@@ -256,6 +265,7 @@ int nmp_step_binned(nmp_engine* eng, int64_t ncol, int64_t ld, const float zsoil
   if (!eng || ncol < 0) return NMP_E_ARG;
   if (ncol == 0) return NMP_OK;
   if (ncol > INT32_MAX && order) return NMP_E_ARG;  // order holds int32 column indices
+  if (!julian_ok(julian, yearlen)) return NMP_E_ARG;
   int rc = check_common(eng, ncol, ld, zsoil, dt, yearlen, state, isnow, static_f, static_i,
                         forcing, diag, diag_level, col_status);
   if (rc != NMP_OK) return rc;
@@ -319,6 +329,10 @@ int nmp_run_out(nmp_engine* eng, int64_t ncol, int64_t ld, const float zsoil[4],
     const int64_t nd = diag_level == NMP_DIAG_FULL ? NMP_NDIAG_FULL : NMP_NDIAG_OUT;
     if (diag_stride < nd * ld) return NMP_E_ARG;
   }
+  // every step's julian (formed below exactly as the launches form it) in range
+  if (!julian_ok(julian0, yearlen) ||
+      !julian_ok(julian0 + (float)(nsteps - 1) * dt / 86400.0f, yearlen))
+    return NMP_E_ARG;
   int rc = check_common(eng, ncol, ld, zsoil, dt, yearlen, state, isnow, static_f, static_i,
                         forcing, diag, diag_level, col_status);
   if (rc != NMP_OK) return rc;
@@ -492,6 +506,7 @@ int sflx_columns(nmp_engine* eng, nmp_sflx_args* cols, int64_t n) {
     if (r.isnow < -NMP_NSNOW || r.isnow > 0) return NMP_E_ARG;
     if (!same_f(r.dt, r0.dt) || !same_f(r.julian, r0.julian) || r.yearlen != r0.yearlen)
       return NMP_E_ARG;
+    if (!julian_ok(r.julian, r.yearlen)) return NMP_E_ARG;
     for (int k = 0; k < NMP_NSOIL; ++k)
       if (!same_f(r.zsoil[k], r0.zsoil[k])) return NMP_E_ARG;
   }

@@ -640,6 +640,40 @@ def test_sflx_columns_rejects_what_the_kernel_cannot_honour(engines):
     assert eng.sflx_columns(mk()) is not None
 
 
+def test_julian_outside_the_year_is_rejected(engines):
+    """The calendar position must be a day of the year, 0 <= julian <=
+    yearlen (the reference's phenology indexes its 12-month LAI/SAI tables
+    with it and reads out of bounds past the year's end): nmp_step, nmp_run
+    (every step's julian0 + s*dt/86400) and nmp_sflx_columns return NMP_E_ARG,
+    and the state is left untouched."""
+    from noahmp_amd import lib as _lib
+    from noahmp_amd.engine import ColumnState
+    from noahmp_amd.params import Params
+    eng = engines([L.CASE_NML_OPTIONS[k] for k in L.OPTION_NAMES])
+    cols = cases.make_columns(256, "mixed", Params.builtin().as_dict(), seed=3, julian=180.0)
+    cs = ColumnState.from_host(cols, DEV)
+    f = torch.as_tensor(cases.forcing_step(cols, 180.0, 366, 0, seed=3), device=DEV)
+    before = cs.state.clone()
+    for jul in (366.5, -0.25, float("nan")):
+        with pytest.raises(_lib.NmpError):
+            eng.step(cs, f, cases.CASE_NML_ZSOIL, 1800.0, jul, 366)
+    # a run whose last step would pass the year's end (365.9 + 4 x 1 h)
+    F = f.unsqueeze(0).repeat(4, 1, 1)
+    with pytest.raises(_lib.NmpError):
+        eng.run(cs, F, cases.CASE_NML_ZSOIL, 3600.0, 365.9, 366, 4)
+    torch.cuda.synchronize()
+    assert torch.equal(cs.state, before)
+    g = load("single_casenml_mixed.npz")
+    r = L.sflx_records(g["state0"][:, :4], g["isnow0"][:4], g["static_f"][:, :4],
+                       g["static_i"][:, :4], g["forcing"][:, :4], g["zsoil"], g["dt"],
+                       np.float32(g["yearlen"]) + 1.0, g["yearlen"])
+    with pytest.raises(_lib.NmpError):
+        engines(g["options"]).sflx_columns(r)
+    # the year's last instant itself is accepted
+    eng.step(cs, f, cases.CASE_NML_ZSOIL, 1800.0, 366.0, 366)
+    torch.cuda.synchronize()
+
+
 def test_sflx_columns_caller_ficeold_vs_reference(engines):
     """nmp_sflx_columns takes FICEOLD as the record carries it (noahmp_sflx's
     intent(in) argument, func.f90:129): melting snow columns whose caller
