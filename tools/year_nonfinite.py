@@ -39,6 +39,7 @@ def main():
     cols = cols.take(coherent_order(cols.lon, cols.static_i, cols.isnow, "lon-snow-type"))
     eng = Engine(P, opts, device=0, precision=4)
     cs = ColumnState.from_host(cols, dev)
+    st_init, isn_init = cols.state.copy(), cols.isnow.copy()
     clim = torch.as_tensor(cases.climate(cols), device=dev).float().contiguous()
     F = torch.empty((chunk, L.NFORCING, n), device=dev)
     vt = cols.static_i[L.STATIC_I.index("VEGTYP")]
@@ -78,6 +79,34 @@ def main():
         for nm in ("TV", "TG", "TAH", "SNEQV", "SNOWH", "CANLIQ", "CANICE", "STC", "SH2O"):
             sl = L.s(nm)
             print(f"  col {c0} {nm}: start {st0[sl, c0].tolist()} gpu {got[sl, 0].tolist()}")
+        # the reference itself (oracle/_ref), stepped from the year's initial
+        # state with the same forcing slices (regenerated: the generator is
+        # stateless): where its first non-finite state value appears, and
+        # whether its state after chunk c equals the GPU's bit for bit
+        import ref
+        ref.configure(otuple)
+        st, isn = st_init[:, sel].copy(), isn_init[sel].copy()
+        first = None
+        Fs = torch.empty((L.NFORCING, n), device=dev)
+        for cc in range(c + 1):
+            j0 = (180.0 + cc * chunk * dt / 86400.0) % yl
+            for s in range(chunk):
+                k = cc * chunk + s
+                jul = float(np.float32(j0) + np.float32(s) * np.float32(dt) / np.float32(86400.0))
+                eng.forcing_synth(clim, jul, yl, seed, k, Fs)
+                fsel = Fs[:, torch.as_tensor(sel, device=dev)].cpu().numpy()
+                st, isn, dg, stat = ref.step(cases.CASE_NML_ZSOIL, dt, yl, jul, st, isn,
+                                             cols.static_f[:, sel], cols.static_i[:, sel], fsel)
+                nf = ~np.isfinite(st[:, 0])
+                if first is None and nf.any():
+                    names = [nm for nm in L.STATE_OFF if nf[L.s(nm)].any()]
+                    first = k
+                    print(f"  reference: first non-finite state at step {k} (julian {jul:.4f}): "
+                          f"{names}; status {int(stat[0])}")
+                    print("  forcing at that step", np.round(fsel[:, 0], 4).tolist())
+        same = bit_equal(got, st).all(0)
+        print(f"  reference after chunk {c}: {int(same.sum())}/{sel.size} columns bit-identical "
+              f"to the GPU")
         return 0
     print("no non-finite STC over the year")
     return 0
