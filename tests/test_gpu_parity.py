@@ -747,6 +747,53 @@ def test_full_size_sample_vs_oracle(engines, oracle_port, kind, ncol, opt_veg, p
         assert ok.mean() >= 0.99, column_mismatch(got, st, 1e-9, 1e-9, STATE_NAMES)[1][:8]
 
 
+def test_bench_window_bit_exact_vs_oracle(engines, oracle_port):
+    """The workload bench.py times, as the driver runs it (`--steps 20
+    --warmup 5`): config #3's 1,048,576 mixed columns in the coherent order,
+    two stream ranges, resident forcing slices, julian wrapped at the year,
+    output every 6th step -- all 25 steps, then a seeded sample of 2,048
+    columns (and the last one) through the C restatement with the same
+    inputs: state, ISNOW and the last output step's fluxes bit for bit."""
+    from noahmp_amd.engine import ColumnState, StreamShards
+    from noahmp_amd.order import coherent_order
+    from noahmp_amd.params import Params
+    P = Params.builtin("STAS", "USGS")
+    opts = [L.CASE_NML_OPTIONS[k] for k in L.OPTION_NAMES]
+    eng = engines(opts)
+    n, dt, yl, seed, nsteps, every = 1 << 20, 1800.0, 366, 1000, 25, 6
+    cols = cases.make_columns(n, "mixed", P.as_dict(), seed=seed, julian=180.0)
+    cols = cols.take(coherent_order(cols.lon, cols.static_i, cols.isnow, "lon-snow-type"))
+    jul = [float(np.float32((180.0 + k * dt / 86400.0) % yl)) for k in range(nsteps)]
+    F = [cases.forcing_step(cols, (180.0 + k * dt / 86400.0) % yl, yl, k, seed=seed)
+         for k in range(nsteps)]
+    cs = ColumnState.from_host(cols, DEV)
+    sh = StreamShards(eng, cs, 2)
+    diag = torch.zeros((L.NDIAG_OUT, n), device=DEV)
+    last = None
+    for k in range(nsteps):
+        out = (k + 1) % every == 0
+        last = k if out else last
+        sh.step(torch.as_tensor(F[k], device=DEV), cases.CASE_NML_ZSOIL, dt, jul[k], yl,
+                diag if out else None, L.DIAG_OUT_LEVEL if out else L.DIAG_NONE)
+    sh.join()
+    torch.cuda.synchronize()
+    idx = np.sort(np.random.default_rng(5).choice(n, 2048, replace=False))
+    idx[-1] = n - 1
+    st, isn = cols.state[:, idx], cols.isnow[idx]
+    for k in range(nsteps):
+        st, isn, dg, _ = oracle_port.step(load_params(), tuple(opts), cases.CASE_NML_ZSOIL, dt, yl,
+                                          jul[k], st, isn, cols.static_f[:, idx],
+                                          cols.static_i[:, idx], F[k][:, idx])
+        if k == last:
+            od = np.stack([dg[L.DIAG_FULL.index(m)] for m in L.DIAG_OUT if m != "T2M"])
+    got = cs.state.cpu().numpy()[:, idx]
+    gd = diag.cpu().numpy()[:, idx]
+    gd = np.stack([gd[i] for i, m in enumerate(L.DIAG_OUT) if m != "T2M"])
+    assert np.array_equal(cs.isnow.cpu().numpy()[idx], isn)
+    ok = bit_equal(got, st).all(0) & bit_equal(gd, od).all(0)
+    assert ok.all(), f"{(~ok).sum()} of {idx.size} sampled columns differ"
+
+
 @pytest.mark.parametrize("kind,opt_veg", [("mixed", 1), ("global", 2)])
 def test_year_trajectory_bit_exact_vs_oracle(engines, oracle_port, kind, opt_veg):
     """A whole year of hourly steps (8,784 = config #5's length) of 256 columns,
