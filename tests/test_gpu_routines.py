@@ -301,3 +301,47 @@ def test_device_fp64_loop_division_range(rt):
     assert rt.rt_dv64(1, a2, b2, q2, i2) == 0
     assert i2[0] == a2[0] / b2[0]
     print("2^1023 divisor:", q2[0], "IEEE", i2[0])
+
+
+@pytest.mark.gpu
+def test_fortran_drop_in_vs_reference(oracle_port):
+    """INTEGRATION.md's Fortran drop-in, run: tests/native/fortran_drop_in.f90
+    (built by __graft_entry__.build() with the module `noahmp_func_mi355x`
+    taken verbatim from INTEGRATION.md) calls `frh2o` and `calhum` with the
+    reference's argument lists, one scalar call per case, and the engine
+    answers through nmp_frh2o_host / nmp_calhum_host.  Its outputs equal the
+    reference routines bit for bit (oracle/_ref, else the pinned
+    restatement)."""
+    import subprocess
+    import tempfile
+    import ref
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    exe = os.path.join(root, "tests", "lib", "fortran_drop_in")
+    tbl = os.path.join(root, "oracle", "_ref", "tbl")
+    if not os.path.exists(exe):
+        pytest.fail(f"{exe} missing: run __graft_entry__.build()")
+    if not os.path.isdir(tbl):
+        pytest.skip("no TBL files beside the oracle (oracle/_ref/tbl) for nmp_read_tables")
+    P, slt, tk, smc, sh2o = frh2o_inputs(512, 17)
+    t, p = calhum_inputs(512, 18)
+    n = tk.size
+    with tempfile.TemporaryDirectory() as td:
+        fin, fout = os.path.join(td, "in.bin"), os.path.join(td, "out.bin")
+        with open(fin, "wb") as f:
+            for a in (np.array([n], np.int32), slt.astype(np.int32), tk, smc, sh2o,
+                      t.astype(np.float32), p.astype(np.float32)):
+                f.write(np.ascontiguousarray(a).tobytes())
+        r = subprocess.run([exe, tbl, fin, fout], capture_output=True, text=True, timeout=120)
+        assert r.returncode == 0, r.stdout + r.stderr
+        out = np.fromfile(fout, np.float32)
+    assert out.size == 3 * n
+    fr, q, d = out[:n], out[n:2 * n], out[2 * n:]
+    if ref.available():
+        ref.configure(tuple(int(x) for x in (1,) * 12))
+        want_fr, _ = ref.frh2o(slt, tk, smc, sh2o)
+        want_q, want_d = ref.calhum(t, p)
+    else:
+        want_fr, _ = oracle_port.frh2o(P, slt, tk, smc, sh2o)
+        want_q, want_d = oracle_port.calhum(t, p)
+    assert bit_equal(fr, want_fr).all(), int((~bit_equal(fr, want_fr)).sum())
+    assert bit_equal(q, want_q).all() and bit_equal(d, want_d).all()
