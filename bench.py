@@ -10,8 +10,9 @@ type -- the order the offline driver gives a grid's land points); --order
 as-generated keeps the generator's shuffled order, the worst case.  One bench step = one noahmp_sflx time step of
 every column (one kernel launch, state resident in HBM); every
 --out-every'th step also writes the 16 output diagnostics and, for N > 1,
-gathers them to rank 0, the writing rank (RCCL over xGMI, --gather root; or
-all-gathers them to every rank with --gather all) on a side stream.
+all-gathers them to every rank (north_star's single RCCL all-gather over
+xGMI, --gather all; or gathers them to rank 0 only, the writing rank, with
+--gather root) on a side stream.
 
 Multi-GPU: one process per GPU, columns statically sharded with no data-path
 collective other than that diagnostics gather; per-GPU work is fixed (weak
@@ -126,10 +127,11 @@ def parse():
     ap.add_argument("--out-every", type=int, default=6,
                     help="output (diag + all-gather) step interval; default 6 = run/case.nml's "
                          "output_frequency '3 hour' at the bench's 1800-s step")
-    ap.add_argument("--gather", default="root", choices=("root", "all"),
-                    help="output-step diagnostics collective for N > 1: 'root' gathers to rank 0, "
-                         "the rank that writes LDASOUT (what the offline driver does); 'all' "
-                         "all-gathers to every rank")
+    ap.add_argument("--gather", default="all", choices=("root", "all"),
+                    help="output-step diagnostics collective for N > 1: 'all' (default) "
+                         "all-gathers to every rank, north_star's single RCCL all-gather over "
+                         "xGMI at output steps; 'root' gathers to rank 0 only, the rank that "
+                         "writes LDASOUT (what the offline driver does)")
     ap.add_argument("--period", type=int, default=48, help="resident forcing slices (cycled)")
     ap.add_argument("--forcing", default="resident", choices=("resident", "device"),
                     help="resident: --period host-generated forcing slices held in HBM and "
@@ -189,31 +191,62 @@ def spawn_ranks(n: int, check_gpus: bool = True) -> int:
                   file=sys.stderr, flush=True)
             return 2
     port = os.environ.get("MASTER_PORT") or str(_free_port())
-    procs = []
-    for r in range(n):
-        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
-                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=port,
-                   NMP_BENCH_SPAWNED="1")
-        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *sys.argv[1:]],
-                                      env=env, start_new_session=True))
+
+    def die_with_parent():
+        # in the child, before exec (nothing has touched the GPU): the kernel
+        # sends SIGTERM to the rank if this launcher dies, even by SIGKILL
+        import ctypes
+        ctypes.CDLL(None, use_errno=True).prctl(1, signal.SIGTERM)  # PR_SET_PDEATHSIG
+
+    procs, live = [], []
+
+    def stop(sig=signal.SIGTERM):
+        for q in live:
+            try:
+                os.killpg(q.pid, sig)
+            except ProcessLookupError:
+                pass
+
+    def forward(signum, _frame):
+        # a signal to the launcher reaches the ranks too (they run in their own
+        # sessions, so a terminal's Ctrl-C or a driver's SIGTERM would not)
+        stop(signum)
+        raise SystemExit(128 + signum)
+
+    old = {s: signal.signal(s, forward) for s in (signal.SIGTERM, signal.SIGINT, signal.SIGHUP)}
     status = 0
-    live = list(procs)
-    while live:
-        for p in list(live):
-            rc = p.poll()
-            if rc is None:
-                continue
-            live.remove(p)
-            if rc != 0 and status == 0:
-                status = rc if rc > 0 else 128 - rc
-                print(f"bench.py: rank {procs.index(p)} exited with {rc}; stopping the job",
-                      file=sys.stderr, flush=True)
-                for q in live:  # a rank blocked in a collective would wait forever
-                    try:
-                        os.killpg(q.pid, signal.SIGTERM)
-                    except ProcessLookupError:
-                        pass
-        time.sleep(0.05)
+    try:
+        for r in range(n):
+            env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                       LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=port,
+                       NMP_BENCH_SPAWNED="1")
+            p = subprocess.Popen([sys.executable, os.path.abspath(__file__), *sys.argv[1:]],
+                                 env=env, start_new_session=True, preexec_fn=die_with_parent)
+            procs.append(p)
+            live.append(p)
+        while live:
+            for p in list(live):
+                rc = p.poll()
+                if rc is None:
+                    continue
+                live.remove(p)
+                if rc != 0 and status == 0:
+                    status = rc if rc > 0 else 128 - rc
+                    print(f"bench.py: rank {procs.index(p)} exited with {rc}; stopping the job",
+                          file=sys.stderr, flush=True)
+                    stop()  # a rank blocked in a collective would wait forever
+            time.sleep(0.05)
+    finally:
+        # any exit path (a signal, an exception, a caller's timeout) takes the
+        # ranks down with it: none may outlive the job holding the GPU
+        stop()
+        for q in live:
+            try:
+                q.wait(timeout=10)
+            except subprocess.TimeoutExpired:
+                stop(signal.SIGKILL)
+        for s_, h in old.items():
+            signal.signal(s_, h)
     return status
 
 
@@ -253,6 +286,10 @@ def main():
         sys.exit(2)
     if os.environ.get("NMP_BENCH_FAIL_RANK") == str(rank):  # test hook: a rank that dies
         sys.exit(3)
+    if os.environ.get("NMP_BENCH_HANG_DIR"):  # test hook: ranks that never finish
+        with open(os.path.join(os.environ["NMP_BENCH_HANG_DIR"], f"rank{rank}.pid"), "w") as f:
+            f.write(str(os.getpid()))
+        time.sleep(600)
     if a.launch_probe:
         return launch_probe(a, world, rank, use_dist)
 

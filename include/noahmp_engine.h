@@ -25,6 +25,8 @@
  * nmp_state_from_aos          layout bridge from noahmp_state_t records
  *                                                           core/module_noahmp_type.f90:10-42
  * nmp_finalize, nmp_strerror  (error path of utils `assert`/`stop`, core/module_noahmp_utils.f90:21-53)
+ * nmp_set_launch_variant, nmp_type_size, nmp_option_set, nmp_set_math,
+ *   nmp_set_cols_per_wave     engine tuning / host layout checks (no reference counterpart)
  *
  * Conventions
  *  - Plain pointers and sizes only.  All per-column arrays are structure of
@@ -54,7 +56,7 @@
 extern "C" {
 #endif
 
-#define NMP_ABI_VERSION 4
+#define NMP_ABI_VERSION 5
 
 /* ---- dimensions (core/module_noahmp_global.f90:9-13) -------------------- */
 #define NMP_NSOIL 4
@@ -226,7 +228,9 @@ enum {
   NMP_E_TABLE = -2,    /* table file missing, block not found, parse error */
   NMP_E_OPTION = -3,   /* option value outside the reference's range      */
   NMP_E_DEVICE = -4,   /* HIP error (no device, launch failure)           */
-  NMP_E_PRECISION = -5 /* precision not 4 or 8                            */
+  NMP_E_PRECISION = -5, /* precision not 4 or 8                           */
+  NMP_E_CALENDAR = -6   /* julian outside [0, yearlen] (split a run at the
+                           year boundary; see nmp_step)                     */
 };
 
 typedef struct nmp_engine nmp_engine;
@@ -246,8 +250,8 @@ int nmp_init(const nmp_params* params, const nmp_options* opts, int device, int 
 /* One noahmp_sflx time step for ncol columns (all pointers device, SoA with
  * leading dimension ld).  zsoil[4] (<0, m) and dt are domain-wide; julian /
  * yearlen are the step's calendar position (noahmp_sflx :67), 0 <= julian <=
- * yearlen, else NMP_E_ARG (outside it the reference's phenology reads its
- * monthly LAI/SAI tables out of bounds).  FICEOLD is
+ * yearlen, else NMP_E_CALENDAR (far enough outside it the reference's
+ * phenology reads its monthly LAI/SAI tables out of bounds).  FICEOLD is
  * derived on device from SNICE/SNLIQ at step start, as an offline driver does.
  * diag may be NULL when diag_level == NMP_DIAG_NONE; col_status is OR-ed
  * (caller zeroes it when it wants a fresh mask). */
@@ -284,7 +288,9 @@ int nmp_rebin(nmp_engine* eng, int64_t ncol, const uint8_t* cost, int32_t* order
  * whose forcing slices are forcing + (s % forcing_period)*forcing_stride
  * (elements, real type; forcing_period 0 = nsteps distinct slices), julian
  * advancing by dt/86400 per step (julian0 + (float)s*dt/86400.0f, every one
- * within [0, yearlen], else NMP_E_ARG: split a run at the year boundary);
+ * within [0, yearlen], else NMP_E_CALENDAR: split a run at the year
+ * boundary, the next year with its own yearlen, as the reference's driver
+ * recomputes the day of year every step);
  * bitwise the same as nsteps nmp_step calls.  diag (if non-NULL) receives the last step only. */
 /* Synthetic forcing for one step, generated on the device (no reference
  * counterpart: the reference reads LDASIN files, run/case.nml:6-7, and ships
@@ -334,7 +340,8 @@ int nmp_state_from_aos(const void* records, int64_t n, int64_t ld, float* state,
  * in place; synchronous.  Replaces a loop of `call noahmp_sflx(...)` over n
  * columns (the per-column entry SURVEY 8b names nmp_sflx_column).
  *  - nsoil must be 4 and nsnow 3; dt, julian, yearlen and zsoil must be the
- *    same in every record of one call (they are launch-wide), else NMP_E_ARG.
+ *    same in every record of one call (they are launch-wide), else NMP_E_ARG;
+ *    julian outside [0, yearlen] is NMP_E_CALENDAR.
  *  - FICEOLD is taken as the record carries it, like noahmp_sflx's
  *    intent(in) argument (the SoA nmp_step path derives it from SNICE/SNLIQ
  *    at step start instead, as the offline and WRF drivers compute it).
@@ -393,7 +400,31 @@ int nmp_set_cols_per_wave(nmp_engine* eng, int cpw);
  * depend on it (DESIGN.md "Compile-time option sets"). */
 int nmp_option_set(nmp_engine* eng, int request);
 
+/* Occupancy instantiation of the step kernel.  The kernel is compiled twice
+ * per option set: at full occupancy (4 waves/SIMD fp32, 2 fp64; spills) and
+ * at half occupancy (2 fp32, 1 fp64; fewer or no spills).  NMP_LAUNCH_AUTO
+ * (the default) picks the half-occupancy kernel for launches whose waves fit
+ * in its slots (csrc/engine.hip small_launch), the full one otherwise;
+ * NMP_LAUNCH_SMALL / NMP_LAUNCH_FULL force one for every launch, so a small
+ * column set can be pushed through the kernel production sizes run (parity
+ * tests of both instantiations).  Env NMP_LAUNCH_VARIANT=auto|small|full sets
+ * the default at nmp_init.  Returns the variant in use, or NMP_E_ARG;
+ * request -1 only queries.  Results do not depend on it.  The fp32 "fast"
+ * math kernel has one instantiation (full) and ignores the setting. */
+#define NMP_LAUNCH_AUTO 0
+#define NMP_LAUNCH_SMALL 1
+#define NMP_LAUNCH_FULL 2
+int nmp_set_launch_variant(nmp_engine* eng, int variant);
+
 int nmp_engine_info(const nmp_engine* eng, int* device, int* precision, nmp_options* opts);
+
+/* sizeof of the ABI's records, for hosts that lay them out themselves (a
+ * Fortran bind(C) type, a ctypes Structure) and check the layout at start-up:
+ * which = NMP_TYPE_PARAMS | NMP_TYPE_OPTIONS | NMP_TYPE_SFLX_ARGS; -1 otherwise. */
+#define NMP_TYPE_PARAMS 0
+#define NMP_TYPE_OPTIONS 1
+#define NMP_TYPE_SFLX_ARGS 2
+int64_t nmp_type_size(int which);
 void nmp_finalize(nmp_engine* eng);
 const char* nmp_strerror(int code);
 int nmp_abi_version(void);

@@ -87,6 +87,9 @@ def check_device_asm(asm_files, verbose: bool = True):
     then silently holds the literal's low 32 bits (tools/llvm_repro/: the fp64
     kernels built without MachineCSE computed exp(x) = inf for x > 0, VERDICT
     r2 item 1).  A build whose text does not assemble is refused."""
+    if not os.path.exists(LLVM_MC):
+        raise RuntimeError(f"device assembly check: llvm-mc not found at {LLVM_MC} (set LLVM_MC "
+                           "to its path, or build with check_asm=False)")
     bad = []
     for a in asm_files:
         r = subprocess.run([LLVM_MC, "-triple=amdgcn-amd-amdhsa", f"-mcpu={ARCH}", "-filetype=null",
@@ -138,10 +141,20 @@ def build(force: bool = False, verbose: bool = True, out: str | None = None,
         for _, c in cmds:
             print("[noahmp build]", " ".join(c), flush=True)
     from concurrent.futures import ThreadPoolExecutor
+    asm_cmds = [x for _, x in asm]
+
+    def compile_one(c):
+        # the asm pass is quiet unless it fails; then its diagnostics are shown
+        quiet = c in asm_cmds
+        r = subprocess.run(c, capture_output=quiet, text=True)
+        if r.returncode != 0:
+            if quiet:
+                sys.stderr.write(r.stdout + r.stderr)
+            raise subprocess.CalledProcessError(r.returncode, c)
+
     jobs = int(os.environ.get("MAX_JOBS", "0")) or min(len(cmds) + len(asm), os.cpu_count() or 1)
     with ThreadPoolExecutor(jobs) as ex:
-        for f in [ex.submit(subprocess.run, c, check=True, capture_output=(c in [x for _, x in asm]))
-                  for _, c in cmds + asm]:
+        for f in [ex.submit(compile_one, c) for _, c in cmds + asm]:
             f.result()
     if asm:
         check_device_asm([a for a, _ in asm], verbose)

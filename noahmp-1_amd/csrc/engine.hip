@@ -26,8 +26,16 @@ struct nmp_engine {
   int cpw;   // columns per wave: 8..64, or 0 = chosen per launch from ncol
   int simds; // SIMDs on the device (CUs x 4)
   int os;    // compiled option set matching opts (sflx_kernel.hip kOptionSet), 0 = none
+  int variant;  // NMP_LAUNCH_AUTO | SMALL | FULL: occupancy instantiation per launch
   nmp_options opts;
   nmp::DevParams* dparams;
+  // the synchronous host entries (nmp_sflx_columns, nmp_*_host): a private
+  // non-blocking stream, so they neither wait for nor stall the caller's
+  // streams, and device scratch kept across calls (grown on demand), so a
+  // scalar call from a Fortran loop pays no allocation
+  hipStream_t hstream;
+  char* scratch;
+  size_t scratch_bytes;
 };
 
 namespace {
@@ -59,6 +67,25 @@ int ensure_device(int dev) {
   return NMP_OK;
 }
 
+// Device scratch of at least nb bytes for a synchronous host entry (the
+// previous contents are not kept).  Growing frees the old block after the
+// engine's host stream has drained it.
+char* host_scratch(nmp_engine* e, size_t nb) {
+  if (nb <= e->scratch_bytes) return e->scratch;
+  if (e->scratch) {
+    (void)hipStreamSynchronize(e->hstream);
+    (void)hipFree(e->scratch);
+    e->scratch = nullptr;
+    e->scratch_bytes = 0;
+  }
+  const size_t want = nb < (1u << 20) ? (size_t)(1u << 20) : nb + nb / 4;
+  void* p = nullptr;
+  if (hipMalloc(&p, want) != hipSuccess) return nullptr;
+  e->scratch = static_cast<char*>(p);
+  e->scratch_bytes = want;
+  return e->scratch;
+}
+
 // Columns per wave: 64 unless set.  Fewer columns per wave (more, partly
 // filled waves for a small column set) was measured slower on config #2
 // (65,536 fp64 columns: 0.158 ms per step at 64, 0.209 at 32, 0.361 at 16,
@@ -69,6 +96,8 @@ int cols_per_wave(const nmp_engine* e, int64_t /*ncol*/) { return e->cpw ? e->cp
 // launch whose waves fit in the slots that kernel leaves (one fp64 / two fp32
 // waves per SIMD) gains nothing from the higher occupancy and pays its spills.
 bool small_launch(const nmp_engine* e, int64_t ncol) {
+  if (e->variant == NMP_LAUNCH_SMALL) return true;
+  if (e->variant == NMP_LAUNCH_FULL) return false;
   const int64_t waves = (ncol + cols_per_wave(e, ncol) - 1) / cols_per_wave(e, ncol);
   return waves <= (int64_t)e->simds * (e->precision == 4 ? 2 : 1);
 }
@@ -129,9 +158,15 @@ int launch(nmp_engine* e, int64_t ncol, int64_t ld, const float zsoil[4], float 
 }
 
 // The calendar position noahmp_sflx accepts: 0 <= julian <= yearlen (NaN
-// fails).  Outside it the reference's phenology indexes its 12-month LAI/SAI
-// tables out of bounds (func.f90 phenology, IT1 = FLOOR(12*(DAY-0.5)/YEARLEN
-// + 0.5) > 12), so such a step has no defined result.
+// fails).  The reference's phenology forms T = 12*DAY/YEARLEN and
+// IT1 = T + 0.5 (integer assignment, truncation), IT2 = IT1 + 1, then wraps
+// only IT1 < 1 -> 12 and IT2 > 12 -> 1 (func.f90:588-594); DAY = JULIAN in the
+// northern hemisphere.  From DAY >= 12.5/12 YEARLEN on, IT1 = 13 indexes
+// LK_LAI12M(13, ...) out of bounds (and below -1.5/12 YEARLEN IT2 = 0), so a
+// step there has no defined result.  The check is the calendar's own range,
+// which also keeps a multi-step run from drifting past the year's end
+// unnoticed: the caller splits the run at the boundary with the next year's
+// yearlen, as the reference's driver recomputes the day of year every step.
 bool julian_ok(float julian, int32_t yearlen) {
   return julian >= 0.0f && julian <= (float)yearlen;
 }
@@ -170,6 +205,8 @@ const char* nmp_strerror(int code) {
     case NMP_E_OPTION: return "physics option out of range";
     case NMP_E_DEVICE: return "HIP device error";
     case NMP_E_PRECISION: return "precision must be 4 or 8";
+    case NMP_E_CALENDAR:
+      return "julian outside [0, yearlen]: split the run at the year boundary";
     default: return "unknown error";
   }
 }
@@ -211,7 +248,20 @@ int nmp_init(const nmp_params* params, const nmp_options* opts, int device, int 
   // NMP_GENERIC_OPTIONS=1: always the run-time-options kernel (A/B tests, timing)
   const char* g = std::getenv("NMP_GENERIC_OPTIONS");
   e->os = (g && std::strcmp(g, "1") == 0) ? 0 : option_set(*opts);
+  // NMP_LAUNCH_VARIANT=small|full: force one occupancy instantiation (parity tests)
+  const char* lv = std::getenv("NMP_LAUNCH_VARIANT");
+  e->variant = !lv                          ? NMP_LAUNCH_AUTO
+               : std::strcmp(lv, "small") == 0 ? NMP_LAUNCH_SMALL
+               : std::strcmp(lv, "full") == 0  ? NMP_LAUNCH_FULL
+                                               : NMP_LAUNCH_AUTO;
   e->dparams = d;
+  e->scratch = nullptr;
+  e->scratch_bytes = 0;
+  if (hipStreamCreateWithFlags(&e->hstream, hipStreamNonBlocking) != hipSuccess) {
+    hipFree(d);
+    delete e;
+    return NMP_E_DEVICE;
+  }
   *out = e;
   return NMP_OK;
 }
@@ -235,6 +285,21 @@ int nmp_option_set(nmp_engine* eng, int request) {
   return eng->os;
 }
 
+int nmp_set_launch_variant(nmp_engine* eng, int variant) {
+  if (!eng || variant < -1 || variant > NMP_LAUNCH_FULL) return NMP_E_ARG;
+  if (variant >= 0) eng->variant = variant;
+  return eng->variant;
+}
+
+int64_t nmp_type_size(int which) {
+  switch (which) {
+    case NMP_TYPE_PARAMS: return (int64_t)sizeof(nmp_params);
+    case NMP_TYPE_OPTIONS: return (int64_t)sizeof(nmp_options);
+    case NMP_TYPE_SFLX_ARGS: return (int64_t)sizeof(nmp_sflx_args);
+    default: return -1;
+  }
+}
+
 int nmp_engine_info(const nmp_engine* eng, int* device, int* precision, nmp_options* opts) {
   if (!eng) return NMP_E_ARG;
   if (device) *device = eng->device;
@@ -249,7 +314,7 @@ int nmp_step(nmp_engine* eng, int64_t ncol, int64_t ld, const float zsoil[4], fl
              int32_t* col_status, void* stream) {
   if (!eng || ncol < 0) return NMP_E_ARG;
   if (ncol == 0) return NMP_OK;
-  if (!julian_ok(julian, yearlen)) return NMP_E_ARG;
+  if (!julian_ok(julian, yearlen)) return NMP_E_CALENDAR;
   int rc = check_common(eng, ncol, ld, zsoil, dt, yearlen, state, isnow, static_f, static_i,
                         forcing, diag, diag_level, col_status);
   if (rc != NMP_OK) return rc;
@@ -265,7 +330,7 @@ int nmp_step_binned(nmp_engine* eng, int64_t ncol, int64_t ld, const float zsoil
   if (!eng || ncol < 0) return NMP_E_ARG;
   if (ncol == 0) return NMP_OK;
   if (ncol > INT32_MAX && order) return NMP_E_ARG;  // order holds int32 column indices
-  if (!julian_ok(julian, yearlen)) return NMP_E_ARG;
+  if (!julian_ok(julian, yearlen)) return NMP_E_CALENDAR;
   int rc = check_common(eng, ncol, ld, zsoil, dt, yearlen, state, isnow, static_f, static_i,
                         forcing, diag, diag_level, col_status);
   if (rc != NMP_OK) return rc;
@@ -332,7 +397,7 @@ int nmp_run_out(nmp_engine* eng, int64_t ncol, int64_t ld, const float zsoil[4],
   // every step's julian (formed below exactly as the launches form it) in range
   if (!julian_ok(julian0, yearlen) ||
       !julian_ok(julian0 + (float)(nsteps - 1) * dt / 86400.0f, yearlen))
-    return NMP_E_ARG;
+    return NMP_E_CALENDAR;
   int rc = check_common(eng, ncol, ld, zsoil, dt, yearlen, state, isnow, static_f, static_i,
                         forcing, diag, diag_level, col_status);
   if (rc != NMP_OK) return rc;
@@ -484,17 +549,6 @@ struct SflxPack {
 };
 static_assert(NMP_NSTATE - NMP_S_TV == 28, "scalar state block");
 
-// one device allocation freed on scope exit (the synchronous host entries)
-struct DevBlock {
-  void* p = nullptr;
-  char* alloc(size_t nb) {
-    return hipMalloc(&p, nb) == hipSuccess ? static_cast<char*>(p) : (p = nullptr, nullptr);
-  }
-  ~DevBlock() {
-    if (p) (void)hipFree(p);
-  }
-};
-
 bool same_f(float a, float b) { return std::memcmp(&a, &b, sizeof(float)) == 0; }
 
 template <class T>
@@ -506,7 +560,7 @@ int sflx_columns(nmp_engine* eng, nmp_sflx_args* cols, int64_t n) {
     if (r.isnow < -NMP_NSNOW || r.isnow > 0) return NMP_E_ARG;
     if (!same_f(r.dt, r0.dt) || !same_f(r.julian, r0.julian) || r.yearlen != r0.yearlen)
       return NMP_E_ARG;
-    if (!julian_ok(r.julian, r.yearlen)) return NMP_E_ARG;
+    if (!julian_ok(r.julian, r.yearlen)) return NMP_E_CALENDAR;
     for (int k = 0; k < NMP_NSOIL; ++k)
       if (!same_f(r.zsoil[k], r0.zsoil[k])) return NMP_E_ARG;
   }
@@ -517,8 +571,8 @@ int sflx_columns(nmp_engine* eng, nmp_sflx_args* cols, int64_t n) {
                nb_i = (size_t)n * sizeof(int32_t);
   const size_t nb_fo = h.fo.size() * sizeof(T);
   const size_t total = nb_st + nb_sf + nb_fc + nb_dg + nb_fo + nb_i * (2 + NMP_NSTATIC_I);
-  char* d = nullptr;
-  if (hipMalloc(&d, total) != hipSuccess) return NMP_E_DEVICE;
+  char* d = host_scratch(eng, total);
+  if (!d) return NMP_E_DEVICE;
   char* p = d;
   auto take = [&](size_t nb) { char* q = p; p += nb; return q; };
   T* d_st = reinterpret_cast<T*>(take(nb_st));
@@ -529,26 +583,27 @@ int sflx_columns(nmp_engine* eng, nmp_sflx_args* cols, int64_t n) {
   int32_t* d_isn = reinterpret_cast<int32_t*>(take(nb_i));
   int32_t* d_status = reinterpret_cast<int32_t*>(take(nb_i));
   int32_t* d_si = reinterpret_cast<int32_t*>(take(nb_i * NMP_NSTATIC_I));
-  int rc = NMP_OK;
-  if (hipMemcpy(d_st, h.st.data(), nb_st, hipMemcpyHostToDevice) != hipSuccess ||
-      hipMemcpy(d_sf, h.sf.data(), nb_sf, hipMemcpyHostToDevice) != hipSuccess ||
-      hipMemcpy(d_fc, h.fc.data(), nb_fc, hipMemcpyHostToDevice) != hipSuccess ||
-      hipMemcpy(d_fo, h.fo.data(), nb_fo, hipMemcpyHostToDevice) != hipSuccess ||
-      hipMemcpy(d_isn, h.isn.data(), nb_i, hipMemcpyHostToDevice) != hipSuccess ||
-      hipMemcpy(d_si, h.si.data(), nb_i * NMP_NSTATIC_I, hipMemcpyHostToDevice) != hipSuccess ||
-      hipMemset(d_status, 0, nb_i) != hipSuccess || hipMemset(d_dg, 0, nb_dg) != hipSuccess)
+  const hipStream_t hs = eng->hstream;
+  const auto up = [&](void* dst, const void* src, size_t nb) {
+    return hipMemcpyAsync(dst, src, nb, hipMemcpyHostToDevice, hs) == hipSuccess;
+  };
+  const auto down = [&](void* dst, const void* src, size_t nb) {
+    return hipMemcpyAsync(dst, src, nb, hipMemcpyDeviceToHost, hs) == hipSuccess;
+  };
+  if (!(up(d_st, h.st.data(), nb_st) && up(d_sf, h.sf.data(), nb_sf) &&
+        up(d_fc, h.fc.data(), nb_fc) && up(d_fo, h.fo.data(), nb_fo) &&
+        up(d_isn, h.isn.data(), nb_i) && up(d_si, h.si.data(), nb_i * NMP_NSTATIC_I) &&
+        hipMemsetAsync(d_status, 0, nb_i, hs) == hipSuccess &&
+        hipMemsetAsync(d_dg, 0, nb_dg, hs) == hipSuccess))
+    return NMP_E_DEVICE;
+  int rc = launch(eng, n, n, r0.zsoil, r0.dt, r0.julian, r0.yearlen, d_st, d_isn, d_sf, d_si, d_fc,
+                  d_dg, NMP_DIAG_FULL, d_status, hs, nullptr, nullptr, d_fo);
+  if (rc == NMP_OK && !(down(h.st.data(), d_st, nb_st) && down(h.dg.data(), d_dg, nb_dg) &&
+                        down(h.isn.data(), d_isn, nb_i) && down(h.status.data(), d_status, nb_i)))
     rc = NMP_E_DEVICE;
-  if (rc == NMP_OK)
-    rc = launch(eng, n, n, r0.zsoil, r0.dt, r0.julian, r0.yearlen, d_st, d_isn, d_sf, d_si, d_fc,
-                d_dg, NMP_DIAG_FULL, d_status, nullptr, nullptr, nullptr, d_fo);
-  if (rc == NMP_OK && (hipDeviceSynchronize() != hipSuccess ||
-                       hipMemcpy(h.st.data(), d_st, nb_st, hipMemcpyDeviceToHost) != hipSuccess ||
-                       hipMemcpy(h.dg.data(), d_dg, nb_dg, hipMemcpyDeviceToHost) != hipSuccess ||
-                       hipMemcpy(h.isn.data(), d_isn, nb_i, hipMemcpyDeviceToHost) != hipSuccess ||
-                       hipMemcpy(h.status.data(), d_status, nb_i, hipMemcpyDeviceToHost) !=
-                           hipSuccess))
-    rc = NMP_E_DEVICE;
-  hipFree(d);
+  // the copies above may still be in flight (pageable host memory): drain the
+  // host stream before the host vectors are read or released
+  if (hipStreamSynchronize(hs) != hipSuccess) rc = NMP_E_DEVICE;
   if (rc != NMP_OK) return rc;
   for (int64_t c = 0; c < n; ++c) h.unpack(cols[c], c);
   return NMP_OK;
@@ -600,28 +655,26 @@ int nmp_frh2o_host(nmp_engine* eng, int64_t n, const int32_t* sltyp, const void*
   if (!sltyp || !tkelv || !smc || !soilwat || !free_water) return NMP_E_ARG;
   if (ensure_device(eng->device) != NMP_OK) return NMP_E_DEVICE;
   const size_t nr = (size_t)n * eng->precision, ni = (size_t)n * sizeof(int32_t);
-  DevBlock d;
-  char* base = d.alloc(4 * nr + 2 * ni);
+  char* base = host_scratch(eng, 4 * nr + 2 * ni);
   if (!base) return NMP_E_DEVICE;
   char *t = base, *m = t + nr, *w = m + nr, *o = w + nr;
   int32_t* s = reinterpret_cast<int32_t*>(o + nr);
   int32_t* st = s + n;
-  if (hipMemcpy(t, tkelv, nr, hipMemcpyHostToDevice) != hipSuccess ||
-      hipMemcpy(m, smc, nr, hipMemcpyHostToDevice) != hipSuccess ||
-      hipMemcpy(w, soilwat, nr, hipMemcpyHostToDevice) != hipSuccess ||
-      hipMemcpy(s, sltyp, ni, hipMemcpyHostToDevice) != hipSuccess ||
-      hipMemset(st, 0, ni) != hipSuccess)
-    return NMP_E_DEVICE;
-  if (nmp::launch_frh2o(eng->precision, eng->math, eng->dparams, n, s, t, m, w, o, st, nullptr) !=
-          hipSuccess ||
-      hipDeviceSynchronize() != hipSuccess ||
-      hipMemcpy(free_water, o, nr, hipMemcpyDeviceToHost) != hipSuccess)
-    return NMP_E_DEVICE;
-  if (col_status) {
-    std::vector<int32_t> bits(n);
-    if (hipMemcpy(bits.data(), st, ni, hipMemcpyDeviceToHost) != hipSuccess) return NMP_E_DEVICE;
+  const hipStream_t hs = eng->hstream;
+  std::vector<int32_t> bits(col_status ? n : 0);
+  bool ok = hipMemcpyAsync(t, tkelv, nr, hipMemcpyHostToDevice, hs) == hipSuccess &&
+            hipMemcpyAsync(m, smc, nr, hipMemcpyHostToDevice, hs) == hipSuccess &&
+            hipMemcpyAsync(w, soilwat, nr, hipMemcpyHostToDevice, hs) == hipSuccess &&
+            hipMemcpyAsync(s, sltyp, ni, hipMemcpyHostToDevice, hs) == hipSuccess &&
+            hipMemsetAsync(st, 0, ni, hs) == hipSuccess &&
+            nmp::launch_frh2o(eng->precision, eng->math, eng->dparams, n, s, t, m, w, o, st, hs) ==
+                hipSuccess &&
+            hipMemcpyAsync(free_water, o, nr, hipMemcpyDeviceToHost, hs) == hipSuccess &&
+            (!col_status ||
+             hipMemcpyAsync(bits.data(), st, ni, hipMemcpyDeviceToHost, hs) == hipSuccess);
+  if (hipStreamSynchronize(hs) != hipSuccess || !ok) return NMP_E_DEVICE;
+  if (col_status)
     for (int64_t i = 0; i < n; ++i) col_status[i] |= bits[i];
-  }
   return NMP_OK;
 }
 
@@ -632,25 +685,29 @@ int nmp_calhum_host(nmp_engine* eng, int64_t n, const void* sfctmp, const void* 
   if (!sfctmp || !sfcprs) return NMP_E_ARG;
   if (ensure_device(eng->device) != NMP_OK) return NMP_E_DEVICE;
   const size_t nr = (size_t)n * eng->precision;
-  DevBlock d;
-  char* base = d.alloc(4 * nr);
+  char* base = host_scratch(eng, 4 * nr);
   if (!base) return NMP_E_DEVICE;
   char *t = base, *p = t + nr, *q = p + nr, *dq = q + nr;
-  if (hipMemcpy(t, sfctmp, nr, hipMemcpyHostToDevice) != hipSuccess ||
-      hipMemcpy(p, sfcprs, nr, hipMemcpyHostToDevice) != hipSuccess)
-    return NMP_E_DEVICE;
-  if (nmp::launch_calhum(eng->precision, eng->math, n, t, p, q2sat ? q : nullptr,
-                         dqsdt2 ? dq : nullptr, nullptr) != hipSuccess ||
-      hipDeviceSynchronize() != hipSuccess ||
-      (q2sat && hipMemcpy(q2sat, q, nr, hipMemcpyDeviceToHost) != hipSuccess) ||
-      (dqsdt2 && hipMemcpy(dqsdt2, dq, nr, hipMemcpyDeviceToHost) != hipSuccess))
-    return NMP_E_DEVICE;
+  const hipStream_t hs = eng->hstream;
+  const bool ok =
+      hipMemcpyAsync(t, sfctmp, nr, hipMemcpyHostToDevice, hs) == hipSuccess &&
+      hipMemcpyAsync(p, sfcprs, nr, hipMemcpyHostToDevice, hs) == hipSuccess &&
+      nmp::launch_calhum(eng->precision, eng->math, n, t, p, q2sat ? q : nullptr,
+                         dqsdt2 ? dq : nullptr, hs) == hipSuccess &&
+      (!q2sat || hipMemcpyAsync(q2sat, q, nr, hipMemcpyDeviceToHost, hs) == hipSuccess) &&
+      (!dqsdt2 || hipMemcpyAsync(dqsdt2, dq, nr, hipMemcpyDeviceToHost, hs) == hipSuccess);
+  if (hipStreamSynchronize(hs) != hipSuccess || !ok) return NMP_E_DEVICE;
   return NMP_OK;
 }
 
 void nmp_finalize(nmp_engine* eng) {
   if (!eng) return;
   ensure_device(eng->device);
+  if (eng->hstream) {
+    (void)hipStreamSynchronize(eng->hstream);
+    (void)hipStreamDestroy(eng->hstream);
+  }
+  if (eng->scratch) hipFree(eng->scratch);
   if (eng->dparams) hipFree(eng->dparams);
   delete eng;
 }

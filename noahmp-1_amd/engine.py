@@ -19,6 +19,8 @@ from . import lib as _lib
 from .params import Params
 
 MATH_REF, MATH_FAST = 0, 1
+# nmp_set_launch_variant: occupancy instantiation of the step kernel
+LAUNCH_VARIANTS = {"auto": 0, "small": 1, "full": 2}
 
 
 def _ptr(t, off: int = 0):
@@ -93,6 +95,15 @@ class Engine:
         rc = self._lib.nmp_option_set(self._h, int(request))
         _lib.check(min(rc, 0), "nmp_option_set")
         return rc
+
+    def launch_variant(self, variant: str | int | None = None) -> str:
+        """nmp_set_launch_variant: "small" / "full" force the half- / full-
+        occupancy kernel for every launch, "auto" (default) picks by column
+        count; None only queries.  Returns the variant in use."""
+        v = -1 if variant is None else LAUNCH_VARIANTS.get(variant, variant)
+        rc = self._lib.nmp_set_launch_variant(self._h, int(v))
+        _lib.check(min(rc, 0), "nmp_set_launch_variant")
+        return {i: k for k, i in LAUNCH_VARIANTS.items()}[rc]
 
     def set_math(self, mode: int):
         _lib.check(self._lib.nmp_set_math(self._h, int(mode)), "nmp_set_math")
@@ -218,6 +229,9 @@ class Engine:
             rt = np.float32 if self.precision == 4 else np.float64
             a = [np.ascontiguousarray(x, rt) for x in (tkelv, smc, sh2o)]
             si = np.ascontiguousarray(sltyp, np.int32)
+            # the library copies n elements of every array: a shorter one would be over-read
+            for x in (*a, si):
+                assert x.shape == (n,), f"frh2o: every input must have shape ({n},), got {x.shape}"
             out = np.empty(n, rt)
             st = status if status is not None else np.zeros(n, np.int32)
             assert st.dtype == np.int32 and st.flags.c_contiguous and st.shape == (n,)
@@ -230,6 +244,11 @@ class Engine:
             assert t.dtype == self.dtype and t.is_contiguous() and t.shape == (n,)
             assert t.device.type == "cuda" and t.device.index == self.device
         assert sltyp.dtype == torch.int32 and sltyp.is_contiguous() and sltyp.shape == (n,)
+        assert sltyp.device.type == "cuda" and sltyp.device.index == self.device, sltyp.device
+        if status is not None:
+            # the kernel ORs int32 bits into n elements of it on the device
+            assert status.dtype == torch.int32 and status.is_contiguous() and status.shape == (n,)
+            assert status.device.type == "cuda" and status.device.index == self.device
         out = torch.empty(n, dtype=self.dtype, device=tkelv.device)
         s = stream if stream is not None else torch.cuda.current_stream(self.device)
         _lib.check(self._lib.nmp_frh2o(self._h, n, _ptr(sltyp), _ptr(tkelv), _ptr(smc), _ptr(sh2o),
@@ -244,6 +263,7 @@ class Engine:
         if isinstance(sfctmp, np.ndarray):
             rt = np.float32 if self.precision == 4 else np.float64
             t, p = (np.ascontiguousarray(x, rt) for x in (sfctmp, sfcprs))
+            assert t.shape == p.shape == (n,), f"calhum: inputs must have shape ({n},)"
             q, d = np.empty(n, rt), np.empty(n, rt)
             _lib.check(self._lib.nmp_calhum_host(self._h, n, C.c_void_p(t.ctypes.data),
                                                  C.c_void_p(p.ctypes.data), C.c_void_p(q.ctypes.data),

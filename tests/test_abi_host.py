@@ -44,7 +44,7 @@ def _enum_values(text):
 
 
 def test_header_functions_exported(engine_lib):
-    decl = set(re.findall(r"^\s*(?:int|void|const char\*)\s+(nmp_\w+)\s*\(", _header(), re.M))
+    decl = set(re.findall(r"^\s*(?:int|int64_t|void|const char\*)\s+(nmp_\w+)\s*\(", _header(), re.M))
     assert decl == set(_lib.EXPORTED_SYMBOLS)
     nm = subprocess.run(["nm", "-D", "--defined-only", _lib.library_path()], capture_output=True,
                         text=True, check=True).stdout
@@ -82,9 +82,16 @@ def test_params_struct_size():
 
 
 def test_abi_version_and_errors(engine_lib):
-    assert engine_lib.nmp_abi_version() == 4
-    for code in (0, -1, -2, -3, -4, -5, -99):
+    assert engine_lib.nmp_abi_version() == 5
+    for code in (0, -1, -2, -3, -4, -5, -6, -99):
         assert engine_lib.nmp_strerror(code)
+    assert b"year boundary" in engine_lib.nmp_strerror(-6)
+    # record sizes a host checks its own layout against (no device needed)
+    assert engine_lib.nmp_type_size(0) == C.sizeof(_lib.NmpParams)
+    assert engine_lib.nmp_type_size(1) == C.sizeof(_lib.NmpOptions) == 48
+    assert engine_lib.nmp_type_size(2) == L.sflx_args_dtype().itemsize
+    assert engine_lib.nmp_type_size(3) == -1
+    assert engine_lib.nmp_set_launch_variant(None, 1) == -1
     p = _lib.NmpParams()
     h = C.c_void_p()
     good = _lib.NmpOptions(*L.options_tuple(L.CASE_NML_OPTIONS))

@@ -75,3 +75,52 @@ def test_bench_two_ranks_on_the_gpu():
     assert ln["n_gpus"] == 2 and ln["config"]["ncol_total"] == 2 * 8192
     assert ln["value"] > 0 and ln["checks"]["stc_finite"]
     assert ln["config"]["backend"] == "gloo"
+
+
+@pytest.mark.parametrize("how", ["SIGTERM", "SIGKILL"])
+def test_launcher_death_takes_the_ranks_down(tmp_path, how):
+    """The ranks run in their own sessions; if the launcher is stopped (a
+    signal, a driver's timeout) or killed outright, no rank may outlive it
+    holding the GPU: SIGTERM is forwarded to every rank's process group, and
+    each rank has PR_SET_PDEATHSIG for the launcher's SIGKILL."""
+    import signal
+    import time
+    e = dict(os.environ, NMP_BENCH_HANG_DIR=str(tmp_path))
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        e.pop(k, None)
+    p = subprocess.Popen([sys.executable, BENCH, "--gpus", "2", "--launch-probe", "--ncol", "100"],
+                         env=e, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+    pids = []
+    for _ in range(600):
+        files = sorted(tmp_path.glob("rank*.pid"))
+        if len(files) == 2 and all(f.read_text() for f in files):
+            pids = [int(f.read_text()) for f in files]
+            break
+        time.sleep(0.1)
+    try:
+        assert len(pids) == 2, "ranks did not start"
+        p.send_signal(getattr(signal, how))
+        p.wait(timeout=30)
+
+        def alive(pid):
+            try:
+                os.kill(pid, 0)
+            except ProcessLookupError:
+                return False
+            # a zombie awaiting its reaper is gone for our purposes
+            try:
+                with open(f"/proc/{pid}/stat") as f:
+                    return f.read().split(")")[-1].split()[0] != "Z"
+            except FileNotFoundError:
+                return False
+        for _ in range(100):
+            if not any(alive(q) for q in pids):
+                break
+            time.sleep(0.1)
+        assert not any(alive(q) for q in pids), "a rank outlived the launcher"
+    finally:
+        for q in pids:
+            try:
+                os.kill(q, signal.SIGKILL)
+            except ProcessLookupError:
+                pass

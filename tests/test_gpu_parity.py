@@ -34,6 +34,12 @@ pytestmark = pytest.mark.gpu
 
 STATE_NAMES = [f"{n}[{k}]" if w > 1 else n for n, w in L.STATE_FIELDS for k in range(w)]
 DEV = "cuda:0"
+# Both occupancy instantiations of the step kernel (nmp_set_launch_variant):
+# "small" is what the fixture sizes select by themselves (half occupancy),
+# "full" the 4-waves/SIMD fp32 / 2-waves fp64 kernel every production-size
+# launch runs.  Register allocation differs between them, so each is pinned
+# to the reference on its own ("What's weak" 1).
+VARIANTS = ["small", "full"]
 
 
 @pytest.fixture(scope="module")
@@ -42,13 +48,14 @@ def engines(engine_lib):
     from noahmp_amd.params import Params
     cache, tables = {}, {}
 
-    def get(options, precision=4, math="ref", tags=("STAS", "USGS")):
-        key = (tuple(int(x) for x in options), precision, math, tuple(tags))
+    def get(options, precision=4, math="ref", tags=("STAS", "USGS"), variant="auto"):
+        key = (tuple(int(x) for x in options), precision, math, tuple(tags), variant)
         if key not in cache:
             if tags not in tables:
                 tables[tags] = Params.builtin(*tags)
             cache[key] = Engine(tables[tags], dict(zip(L.OPTION_NAMES, key[0])), device=0,
                                 precision=precision, math=math)
+            assert cache[key].launch_variant(variant) == variant
         return cache[key]
     return get
 
@@ -81,13 +88,17 @@ def test_single_call_vs_reference(engines, name):
     assert not msg, f"{name}: {msg}"
 
 
+@pytest.mark.parametrize("variant", VARIANTS)
 @pytest.mark.parametrize("name", single_names())
-def test_single_call_bit_exact_vs_reference(engines, name):
+def test_single_call_bit_exact_vs_reference(engines, name, variant):
     """Default ("ref") math = glibc's float libm restated bit-exactly
     (csrc/glibc_math.h), so the kernel must reproduce the reference Fortran
-    bit for bit: every state field, every one of the 58 outputs, ISNOW, status."""
+    bit for bit: every state field, every one of the 58 outputs, ISNOW, status
+    -- in both occupancy instantiations of every option-set kernel the
+    fixture's options select (set 1, set 2 or the run-time-options set 0)."""
     g = load(f"single_{name}.npz")
-    st, isn, dg, status = run_single(engines(g["options"], tags=fixture_tags(g)), g)
+    st, isn, dg, status = run_single(
+        engines(g["options"], tags=fixture_tags(g), variant=variant), g)
     exact = bit_equal(st, g["state1"]).all(0) & bit_equal(dg, g["diag"]).all(0) & \
         (isn == g["isnow1"]) & (as_ref_status(status) == g["status"])
     _, rep_s = column_mismatch(st, g["state1"], 0, 0, STATE_NAMES)
@@ -111,8 +122,9 @@ def test_single_call_fp64_vs_fp64_oracle(engines, oracle_port, name):
     assert ok.mean() >= 0.99 or (~ok).sum() <= 1, "; ".join(rep_s[:8] + rep_d[:8])
 
 
+@pytest.mark.parametrize("variant", VARIANTS)
 @pytest.mark.parametrize("name", single_names())
-def test_single_call_fp64_vs_reference(engines, name):
+def test_single_call_fp64_vs_reference(engines, name, variant):
     """fp64 engine vs the fp32 REFERENCE fixtures at SURVEY 8c's x10 bar on all
     56 state values and all 58 outputs (golden_io.parity_fp64_vs_reference):
     >= 97 % of non-tie columns inside the bar, at most one column outside the
@@ -120,7 +132,8 @@ def test_single_call_fp64_vs_reference(engines, name):
     (test_oracle_golden.py::test_fp64_restatement_vs_fp32_reference) shows the
     misses are Newton/bisection loops exiting on another iteration in fp64."""
     g = load(f"single_{name}.npz")
-    out = run_single(engines(g["options"], 8, tags=fixture_tags(g)), g, torch.float64)
+    out = run_single(engines(g["options"], 8, tags=fixture_tags(g), variant=variant), g,
+                     torch.float64)
     r, miss, env_miss, rep = parity_fp64_vs_reference(*out, g)
     print(name, r)
     assert r["frac"] >= FP64_TOL_FRAC, (name, r, rep[:8])
@@ -141,13 +154,14 @@ def test_single_call_fp64_vs_reference_pooled(engines):
     assert tot["env_miss"] <= 2, tot
 
 
+@pytest.mark.parametrize("variant", VARIANTS)
 @pytest.mark.parametrize("name", ["casenml", "combo_a", "snow"])
-def test_trajectory_fp64_vs_reference(engines, name):
+def test_trajectory_fp64_vs_reference(engines, name, variant):
     """fp64 engine along the reference trajectories at the x10 bar
     (golden_io.check_fp64_trajectory_step): the run/case.nml column inside
     rel 1e-3 at every saved step, snow by domain means within 1 %."""
     g = load(f"traj_{name}.npz")
-    out = _trajectory(engines(g["options"], 8), g, torch.float64)
+    out = _trajectory(engines(g["options"], 8, variant=variant), g, torch.float64)
     for k, (st, isn, dg, _) in enumerate(out):
         step = min((k + 1) * int(g["keep_every"]) - 1, g["forcing"].shape[0] - 1)
         check_fp64_trajectory_step(name, step, st, isn, dg, g, k)
@@ -218,10 +232,11 @@ def _trajectory(eng, g, dtype=torch.float32):
     return out
 
 
-def test_trajectory_casenml(engines):
+@pytest.mark.parametrize("variant", VARIANTS)
+def test_trajectory_casenml(engines, variant):
     """96 steps of the case.nml column + 31 mixed columns vs the reference run."""
     g = load("traj_casenml.npz")
-    out = _trajectory(engines(g["options"]), g)
+    out = _trajectory(engines(g["options"], variant=variant), g)
     for k in range(0, len(out), 8):
         st, isn = out[k][0], out[k][1]
         exp = g["states"][k]
@@ -238,10 +253,11 @@ def test_trajectory_casenml(engines):
         assert ex.all(), (k, ex.mean())
 
 
-def test_trajectory_snow_distribution(engines):
+@pytest.mark.parametrize("variant", VARIANTS)
+def test_trajectory_snow_distribution(engines, variant):
     """480 snow steps: domain means (SWE, depth, cover) within 1 %, as SURVEY 8c asks."""
     g = load("traj_snow.npz")
-    out = _trajectory(engines(g["options"]), g)
+    out = _trajectory(engines(g["options"], variant=variant), g)
     for k, (st, isn, dg, _) in enumerate(out):
         exp = g["states"][k]
         for f in ("SNEQV", "SNOWH"):
@@ -256,12 +272,13 @@ def test_trajectory_snow_distribution(engines):
         assert ex.all(), (k, ex.mean())
 
 
-def test_trajectory_option_combo(engines):
+@pytest.mark.parametrize("variant", VARIANTS)
+def test_trajectory_option_combo(engines, variant):
     """48 steps under combo_a (dynamic vegetation + carbon, Jarvis canopy
     resistance, Chen97 surface layer, ... -- tests/golden/make_golden.py):
     bit-exact to the reference at every step."""
     g = load("traj_combo_a.npz")
-    out = _trajectory(engines(g["options"]), g)
+    out = _trajectory(engines(g["options"], variant=variant), g)
     for k, (st, isn, dg, status) in enumerate(out):
         ex = bit_equal(st, g["states"][k]).all(0) & (isn == g["isnows"][k]) & \
             bit_equal(dg, g["diags"][k]).all(0) & (as_ref_status(status) == g["statuses"][k])
@@ -465,6 +482,81 @@ def test_option_set_kernels_equal_generic(opt_veg, precision):
     c_eng = Engine(tab, dict(opts, opt_run=2), device=0, precision=precision)
     assert c_eng.option_set() == 0
     c_eng.close()
+
+
+def _combo_options(name):
+    return [int(x) for x in load(f"single_combo_{name}.npz")["options"]]
+
+
+@pytest.mark.parametrize("precision", [4, 8])
+@pytest.mark.parametrize("optset", ["set1", "set2", "set0_casenml", "set0_combo_a",
+                                    "set0_combo_b", "set0_combo_c"])
+def test_full_and_small_kernels_equal(optset, precision):
+    """The full-occupancy kernel (what every production-size launch runs) ==
+    the half-occupancy kernel (what the fixture sizes select), bitwise, for
+    every compiled option set and for the run-time-options kernel under
+    case.nml and under the hand-picked option combinations (which together set
+    every option to a non-default value): 4 steps of 200,003 mixed columns
+    (ragged), full diagnostics on alternate steps.  Round 3's ballot build got
+    91,067 columns wrong in exactly this comparison while every fixture test
+    (half occupancy) passed."""
+    from noahmp_amd.engine import ColumnState, Engine
+    from noahmp_amd.params import Params
+    n = 200_003
+    if optset.startswith("set0_combo"):
+        opts = dict(zip(L.OPTION_NAMES, _combo_options(optset[len("set0_combo_"):])))
+    else:
+        opts = dict(L.CASE_NML_OPTIONS, opt_veg=2 if optset == "set2" else 1)
+    tab = Params.builtin()
+    engs = [Engine(tab, opts, device=0, precision=precision) for _ in range(2)]
+    try:
+        if optset.startswith("set0"):
+            for e in engs:
+                e.option_set(0)
+        assert engs[0].option_set() == {"set1": 1, "set2": 2}.get(optset, 0)
+        assert engs[0].launch_variant("small") == "small"
+        assert engs[1].launch_variant("full") == "full"
+        dtype = torch.float32 if precision == 4 else torch.float64
+        cols = cases.make_columns(n, "mixed", tab.as_dict(), seed=13, julian=60.0)
+        F = [torch.as_tensor(cases.forcing_step(cols, 60.0 + s / 48.0, 365, s, seed=13),
+                             device=DEV).to(dtype) for s in range(4)]
+        cs = [ColumnState.from_host(cols, DEV, dtype) for _ in range(2)]
+        nbytes = torch.int8
+        for s in range(4):
+            lvl = L.DIAG_FULL_LEVEL if s % 2 else L.DIAG_NONE
+            d = [torch.zeros((L.NDIAG_FULL, n), dtype=dtype, device=DEV) if s % 2 else None
+                 for _ in range(2)]
+            for e, c, dd in zip(engs, cs, d):
+                e.step(c, F[s], cases.CASE_NML_ZSOIL, 1800.0, 60.0 + s / 48.0, 365, dd, lvl)
+            torch.cuda.synchronize()
+            if s % 2:
+                diff = (d[0].view(nbytes) != d[1].view(nbytes)).any(0).sum().item()
+                assert diff == 0, f"step {s}: {diff} columns' diagnostics differ"
+        bad = (cs[0].state.view(nbytes) != cs[1].state.view(nbytes)).any(0)
+        assert not bool(bad.any()), f"{int(bad.sum())} columns' state differ"
+        assert torch.equal(cs[0].isnow, cs[1].isnow) and torch.equal(cs[0].status, cs[1].status)
+    finally:
+        for e in engs:
+            e.close()
+
+
+def test_launch_variant_auto_picks_by_size(engines):
+    """auto: the half-occupancy kernel for launches within its wave slots, the
+    full one above; small/full stick for every size; bad requests are refused."""
+    from noahmp_amd import lib as _lib
+    from noahmp_amd.engine import Engine
+    from noahmp_amd.params import Params
+    e = Engine(Params.builtin(), L.CASE_NML_OPTIONS, device=0)
+    try:
+        assert e.launch_variant() == "auto"
+        assert e.launch_variant("full") == "full" and e.launch_variant() == "full"
+        assert e.launch_variant("small") == "small"
+        assert e.launch_variant("auto") == "auto"
+        with pytest.raises(_lib.NmpError):
+            e.launch_variant(3)
+        assert e.launch_variant() == "auto"
+    finally:
+        e.close()
 
 
 @pytest.mark.parametrize("cpw", [8, 24, 40, 64])
@@ -794,8 +886,9 @@ def test_bench_window_bit_exact_vs_oracle(engines, oracle_port):
     assert ok.all(), f"{(~ok).sum()} of {idx.size} sampled columns differ"
 
 
+@pytest.mark.parametrize("variant", VARIANTS)
 @pytest.mark.parametrize("kind,opt_veg", [("mixed", 1), ("global", 2)])
-def test_year_trajectory_bit_exact_vs_oracle(engines, oracle_port, kind, opt_veg):
+def test_year_trajectory_bit_exact_vs_oracle(engines, oracle_port, kind, opt_veg, variant):
     """A whole year of hourly steps (8,784 = config #5's length) of 256 columns,
     bit for bit against the fp32 C restatement (itself bit-exact to the
     reference on every fixture): state, ISNOW and the output fluxes compared
@@ -809,7 +902,7 @@ def test_year_trajectory_bit_exact_vs_oracle(engines, oracle_port, kind, opt_veg
     P = Params.builtin()
     opts = dict(L.CASE_NML_OPTIONS, opt_veg=opt_veg)
     otuple = tuple(opts[k] for k in L.OPTION_NAMES)
-    eng = engines(otuple, 4)
+    eng = engines(otuple, 4, variant=variant)
     n, dt, nsteps, nchunk, yl = 256, 3600.0, 8784, 12, 366
     cols = cases.make_columns(n, kind, P.as_dict(), seed=29, julian=0.0)
     F = np.stack([cases.forcing_step(cols, s * dt / 86400.0, yl, s, seed=29) for s in range(nsteps)])
