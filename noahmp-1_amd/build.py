@@ -19,7 +19,8 @@ DEFAULT_LIB_PATH = os.path.join(LIB_DIR, "libnoahmp_engine.so")
 LIB_PATH = os.environ.get("NOAHMP_ENGINE_LIB") or DEFAULT_LIB_PATH
 SOURCES = ["engine.hip", "sflx_kernel.hip", "sflx_kernel_f64.hip", "rebin.hip", "forcing.hip",
            "routines.hip", "tables.cpp"]
-HEADERS = ["dev_params.h", "sflx_kargs.h", "sflx_math.h", "sflx_routines.h", "glibc_math.h"]
+HEADERS = ["dev_params.h", "sflx_kargs.h", "sflx_math.h", "sflx_routines.h", "glibc_math.h",
+           "vege_domain.h"]
 # per-source flags: sflx_kernel.hip is compiled as the fp32 translation unit,
 # sflx_kernel_f64.hip (the same file, NMP_TU 8) as the fp64 one, in parallel.
 # The fp64 unit can take its own flags (tools/build_variants.py f64*): with

@@ -26,6 +26,7 @@
 #include "sflx_kargs.h"
 #include "sflx_math.h"
 #include "sflx_routines.h"
+#include "vege_domain.h"
 
 namespace nmp {
 
@@ -929,9 +930,18 @@ struct PhaseClock {
 static __device__ unsigned long long nmp_wave_rec[4 * NMP_WAVE_REC_MAX];
 static __device__ unsigned int nmp_wave_ctr;
 #endif
+#ifdef NMP_COUNT_FALLBACK
+static __device__ unsigned int nmp_fallback_ctr;
+static __device__ unsigned int nmp_fb_reason[32];
+#endif
 
 
 // Unroll factor of the vege_flux Newton loop (tuning knob, results identical).
+// NMP_VEGE_DIV: the canopy Newton loop divides with DivFast32 where its range
+// proofs hold (fp32 "ref" option-set kernels), IEEE otherwise
+#ifndef NMP_VEGE_DIV
+#define NMP_VEGE_DIV 1
+#endif
 #ifndef NMP_VEGE_UNROLL
 #define NMP_VEGE_UNROLL 1
 #endif
@@ -1337,10 +1347,69 @@ DEV void sflx_column(const DevParams& P, const KArgs<T>& A, Col<T>& c, const Sin
     // EVC's limit CANLIQ*LATHEAV/DT or CANICE*LATHEAV/DT (:2860-2864): both
     // loop-invariant, the iteration picks one by the canopy temperature
     T evlim_liq = dv(c.canliq * latheav, DT), evlim_ice = dv(c.canice * latheav, DT);
+    // The loop-invariant half of the range proof's domain (vege_domain.h,
+    // tools/div_proof.py), evaluated once per column before the loop; NaN
+    // fails every comparison.
+#ifdef NMP_COUNT_FALLBACK
+    // (probe builds) which condition sent the lane to the IEEE loop
+    unsigned fb_why = 0;
+#define NMP_DOM(flag, bit, cond)                 \
+  do {                                           \
+    const bool c_ = (cond);                      \
+    flag = flag & c_;                            \
+    if (!c_) fb_why |= 1u << (bit);              \
+  } while (0)
+#else
+#define NMP_DOM(flag, bit, cond) flag = flag & (cond)
+#endif
+    auto vege_domain_ok = [&]() -> bool {
+      auto in = [](T x, double lo, double hi) { return x >= (T)lo && x <= (T)hi; };
+      auto zero_or = [&](T x, double lo, double hi) { return x == L(0.0) || in(x, lo, hi); };
+      bool k = true;
+      NMP_DOM(k, 0, in(c.sfctmp, NMP_DOM_T_LO, NMP_DOM_T_HI) & in(c.tg, NMP_DOM_T_LO, NMP_DOM_T_HI));
+      NMP_DOM(k, 1, in(qair, 0.0, 1.0) & in(rhoair, NMP_DOM_RHO_LO, NMP_DOM_RHO_HI));
+      NMP_DOM(k, 2, in(c.sfcprs, NMP_DOM_P_LO, NMP_DOM_P_HI) & in(eair, 0.0, NMP_DOM_EAIR_HI));
+      NMP_DOM(k, 3, in(ur, 1.0, NMP_DOM_UR_HI));
+      NMP_DOM(k, 4, in(lgv.tmpcm, NMP_DOM_TMPC_LO, NMP_DOM_TMPC_HI) &
+                        in(lgv.tmpch, NMP_DOM_TMPC_LO, NMP_DOM_TMPC_HI) &
+                        in(lgv.tmpcm2, NMP_DOM_TMPC_LO, NMP_DOM_TMPC_HI) &
+                        in(lgv.tmpch2, NMP_DOM_TMPC_LO, NMP_DOM_TMPC_HI));
+      NMP_DOM(k, 5, in(zlvl - zpd, NMP_DOM_DZ_LO, NMP_DOM_DZ_HI));
+      NMP_DOM(k, 6, in(hcan, NMP_DOM_HCAN_LO, NMP_DOM_HCAN_HI) &
+                        in(z0m, NMP_DOM_Z0_LO, NMP_DOM_Z0_HI) &
+                        in(z0mg, NMP_DOM_Z0_LO, NMP_DOM_Z0_HI) &
+                        zero_or(zpd, NMP_DOM_Z0_LO, NMP_DOM_HCAN_HI));
+      NMP_DOM(k, 7, (zpd <= hcan) & (z0mg <= hcan) & (z0m + zpd <= L(2.0) * hcan));
+      NMP_DOM(k, 8, in(cwp * vaie * hcan, NMP_DOM_CWPH_LO, NMP_DOM_CWPH_HI));
+      NMP_DOM(k, 9, in(vaie, NMP_DOM_VAI_LO, 6.0));
+      NMP_DOM(k, 10, zero_or(laisune, NMP_DOM_LAI_LO, 6.0) & zero_or(laishae, NMP_DOM_LAI_LO, 6.0));
+      NMP_DOM(k, 11, zero_or(c.fwet, NMP_DOM_FWET_LO, 1.0));
+      NMP_DOM(k, 12, in(fveg, NMP_DOM_FVEG_LO, 1.0));
+      NMP_DOM(k, 13, in(sqrt_dleaf_uc, NMP_DOM_SDL_LO, NMP_DOM_SDL_HI));
+      NMP_DOM(k, 14, in(rsurf, 0.0, NMP_DOM_RSURF_HI));
+#ifdef NMP_VD_NODOMAIN
+      k = true;  // (timing probe only: not exact in general)
+#endif
+      return k;
+    };
     // The whole canopy Newton loop (loop1, func.f90:2744-2877) with the
     // division policy `d` (sflx_math.h): every loop variable starts here, so a
     // lane can run it again with the reference's divisions.
-    auto vege_loop = [&](auto& d) {
+    auto vege_loop = [&](auto& d) -> bool {
+      constexpr bool kFast = !std::is_same<std::decay_t<decltype(d)>, DivRef<T>>::value;
+      // CTR, TR and DTV keep IEEE division under every policy: their
+      // numerators are products of several possibly small factors, outside
+      // what the range proof bounds (tools/div_proof.py)
+#ifdef NMP_VD_ALLFAST
+      auto& dref = d;  // (timing probe only: not exact in general)
+#else
+      const DivRef<T> dref;
+#endif
+      // the per-iteration windows of the range proof (vege_domain.h): TV at
+      // the start of every iteration, RAHG after every ragrb, RSSUN/RSSHA after
+      // the first iteration; any miss sends the lane through the IEEE loop
+      bool ok = true;
+      auto in = [](T x, T lo, T hi) { return x >= lo && x <= hi; };
       cmv = c.cm;
       chv = c.ch;
       fv = L(0.1); h = L(0.0); hg = L(0.0);
@@ -1376,6 +1445,9 @@ DEV void sflx_column(const DevParams& P, const KArgs<T>& A, Col<T>& c, const Sin
         const Recip<T> rrahc = d.rec(rahc);  // RAWC = RAHC: CAH = CAW, H share it
         ragrb<T, R>(d, inv.rhocp, rhcan, dzg, sqrt_dleaf_uc, iter, vaie, hg, c.tah, zpd, z0mg, hcan,
                     z0h, fv, cwp, mpe, fhg, rahg, rb);
+#ifndef NMP_VD_NOWIN
+        if constexpr (kFast) NMP_DOM(ok, 16, in(rahg, (T)NMP_DOM_RAHG_LO, (T)NMP_DOM_RAHG_HI));
+#endif
         const Recip<T> rrahg = d.rec(rahg), rrb = d.rec(rb);  // RAWG = RAHG
         T estv, destv;
         esat_sel(tdc(c.tv), estv, destv);
@@ -1391,6 +1463,10 @@ DEV void sflx_column(const DevParams& P, const KArgs<T>& A, Col<T>& c, const Sin
             canres<T, R>(V, c.sfcprs, c.tv, parsun, c.eah, btran, rssun, psnsun);
             canres<T, R>(V, c.sfcprs, c.tv, parsha, c.eah, btran, rssha, psnsha);
           }
+#ifndef NMP_VD_NOWIN
+          if constexpr (kFast)
+            NMP_DOM(ok, 17, in(rssun, L(0.0), (T)NMP_DOM_RS_HI) & in(rssha, L(0.0), (T)NMP_DOM_RS_HI));
+#endif
         }
         cah = d.divk(L(1.0), rrahc);
         cvh = d.divk(two_vaie, rrb);
@@ -1410,17 +1486,17 @@ DEV void sflx_column(const DevParams& P, const KArgs<T>& A, Col<T>& c, const Sin
         T aea = d.div(eair * caw + estg * cgw, rcond2);
         T bea = d.div(cew + ctw, rcond2);
         T cev = d.div((L(1.0) - bea) * cew * rhoair * CPAIR, rgammav);
-        T ctr = d.div((L(1.0) - bea) * ctw * rhoair * CPAIR, rgammav);
+        T ctr = dref.div((L(1.0) - bea) * ctw * rhoair * CPAIR, rgammav);
         c.tah = ata + bta * c.tv;
         c.eah = aea + bea * estv;
         irc = fveg * (air + cir * p4(c.tv));
         shc = fveg * rhoair * CPAIR * cvh * (c.tv - c.tah);
         evc = d.div(fveg * rhoair * CPAIR * cew * (estv - c.eah), rgammav);
-        tr = d.div(fveg * rhoair * CPAIR * ctw * (estv - c.eah), rgammav);
+        tr = dref.div(fveg * rhoair * CPAIR * ctw * (estv - c.eah), rgammav);
         evc = rmin((c.tv > TFRZ) ? evlim_liq : evlim_ice, evc);
         T b = sav - irc - shc - evc - tr;
         T a = fveg * (L(4.0) * cir * p3(c.tv) + csh + (cev + ctr) * destv);
-        T dtv = d.div(b, d.rec(a));
+        T dtv = dref.div(b, dref.rec(a));
         irc = irc + fveg * L(4.0) * cir * p3(c.tv) * dtv;
         shc = shc + fveg * csh * dtv;
         evc = evc + fveg * cev * destv * dtv;
@@ -1431,18 +1507,44 @@ DEV void sflx_column(const DevParams& P, const KArgs<T>& A, Col<T>& c, const Sin
         c.qsfc = d.div(L(0.622) * c.eah, d.rec(c.sfcprs - L(0.378) * c.eah));
         return dtv;
       };
+      auto tv_in_window = [&]() { return in(c.tv, (T)NMP_DOM_T_LO, (T)NMP_DOM_T_HI); };
+      if constexpr (kFast) NMP_DOM(ok, 18, tv_in_window());
       vtrips = 1;
       vege_iter(1, std::true_type{});  // iter 1 cannot exit (the test needs iter >= 5)
       NMP_UNROLL(NMP_VEGE_UNROLL)
       for (int iter = 2; iter <= 20; ++iter) {
         vtrips = iter;
+        if constexpr (kFast) NMP_DOM(ok, 19, tv_in_window());
         const T dtv = vege_iter(iter, std::false_type{});
         if (liter == 1) break;
         if (iter >= 5 && fabs(dtv) <= L(0.01) && liter == 0) liter = 1;
       }
+      return ok;
     };
     DivRef<T> dr;
+#if NMP_VEGE_DIV
+    if constexpr (sizeof(T) == 4 && R && OS != 0) {
+      // the short exact division wherever the range proofs hold; a lane
+      // outside their window repeats the loop from its start with IEEE
+      // division (TV/TAH/EAH reloaded: nothing has stored them yet)
+      DivFast32 df;
+      if (!(vege_domain_ok() & vege_loop(df))) {
+#ifdef NMP_COUNT_FALLBACK
+        atomicAdd(&nmp_fallback_ctr, 1u);
+        for (int b = 0; b < 20; ++b)
+          if (fb_why & (1u << b)) atomicAdd(&nmp_fb_reason[b], 1u);
+#endif
+        c.tv = out.ls(NMP_S_TV);
+        c.tah = out.ls(NMP_S_TAH);
+        c.eah = out.ls(NMP_S_EAH);
+        vege_loop(dr);
+      }
+    } else {
+      vege_loop(dr);
+    }
+#else
     vege_loop(dr);
+#endif
     // under-canopy fluxes and TG (loop2, :2881-2914)
     air = -emg * (L(1.0) - emv) * c.lwdn - emg * emv * SB * p4(c.tv);
     cir = emg * SB;
@@ -2993,6 +3095,25 @@ extern "C" int nmp_debug_phase_cycles(unsigned long long* out16, int reset) {
 #endif
 
 
+
+#if defined(NMP_COUNT_FALLBACK) && (!defined(NMP_TU) || NMP_TU == 4)
+// (probe builds) lanes that left the range proof's domain and re-ran the
+// canopy loop with IEEE division since the last reset
+extern "C" long long nmp_debug_fallback_count(int reset, unsigned int* why32) {
+  unsigned int n = 0;
+  if (hipMemcpyFromSymbol(&n, HIP_SYMBOL(nmp_fallback_ctr), sizeof(n)) != hipSuccess) return -4;
+  if (why32 && hipMemcpyFromSymbol(why32, HIP_SYMBOL(nmp_fb_reason), 32 * sizeof(unsigned int)) !=
+                   hipSuccess)
+    return -4;
+  if (reset) {
+    const unsigned int z[32] = {0};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(nmp_fallback_ctr), z, sizeof(unsigned int)) != hipSuccess ||
+        hipMemcpyToSymbol(HIP_SYMBOL(nmp_fb_reason), z, sizeof(z)) != hipSuccess)
+      return -4;
+  }
+  return n;
+}
+#endif
 
 #if defined(NMP_WAVE_TIMING) && (!defined(NMP_TU) || NMP_TU == 4)
 // the fp32 kernels' wave records: copies min(count, max_rec) records of 4 u64

@@ -225,6 +225,33 @@ struct DivRef {
   __device__ __forceinline__ void chk(T) const {}
 };
 
+// DivFast32: the short exact sequence, used where the operands are proven to
+// lie in its exact region (DESIGN.md "Division in the canopy loop").  The
+// reciprocal r = fma(fma(-b, r0, 1), r0, r0) from v_rcp_f32 (shared by every
+// division by the same b), then q = a*r, one fma residual correction and
+// v_div_fixup_f32, which gives zero, infinite and NaN operands their IEEE
+// results.  It equals IEEE a/b bit for bit whenever b is normal with a normal
+// reciprocal, the residual a - b*q is not subnormal (a = 0 or |a| >= 2^-102)
+// and the quotient is normal (tools/fdiv_exhaust.hip: every normal b, every
+// pair of significands, exact scaling by powers of two;
+// profiles/r03/fdiv_exhaust2.txt).
+struct DivFast32 {
+  __device__ __forceinline__ Recip<float> rec(float b) const {
+    float r = __builtin_amdgcn_rcpf(b);
+    const float e = __builtin_fmaf(-b, r, 1.0f);
+    r = __builtin_fmaf(e, r, r);
+    return {b, r};
+  }
+  __device__ __forceinline__ float div(float a, const Recip<float>& R) const {
+    float q = a * R.r;
+    const float e = __builtin_fmaf(-R.b, q, a);
+    q = __builtin_fmaf(e, R.r, q);
+    return __builtin_amdgcn_div_fixupf(q, R.b, a);
+  }
+  __device__ __forceinline__ float divk(float a, const Recip<float>& R) const { return div(a, R); }
+  __device__ __forceinline__ void chk(float) const {}
+};
+
 // Register-array access with a runtime index, lowered to a select chain so the
 // array itself stays in VGPRs (a dynamic subscript would demote it to scratch).
 // The empty asm pins each element as a register value: without it InstCombine

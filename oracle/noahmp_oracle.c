@@ -39,6 +39,47 @@ void oracle_set_stats(int32_t* buf) { g_stats = buf; }
 #define ITER_STAT(k) ((void)0)
 #endif
 
+/* Division operand ranges of the canopy Newton loop (vege_flux with sfcdif1
+ * and ragrb; build with -DORACLE_DIV_STATS only, tools/div_ranges.py): per
+ * site the smallest / largest |a|, |b|, |a/b| over nonzero finite values and
+ * the count of zero numerators.  The arithmetic is unchanged: DV(k, a, b) is
+ * a / b. */
+#ifdef ORACLE_DIV_STATS
+#define NDIVSITE 40
+static double g_div[NDIVSITE][8];
+static int g_div_init;
+void oracle_div_stats(double* out, int reset) {
+  if (!g_div_init || reset) {
+    for (int k = 0; k < NDIVSITE; ++k) {
+      g_div[k][0] = g_div[k][2] = g_div[k][4] = INFINITY;
+      g_div[k][1] = g_div[k][3] = g_div[k][5] = 0.0;
+      g_div[k][6] = g_div[k][7] = 0.0;
+    }
+    g_div_init = 1;
+  }
+  if (out) memcpy(out, g_div, sizeof(g_div));
+}
+static inline void div_rec(int k, double v, int slot) {
+  v = fabs(v);
+  if (v == 0.0 || !isfinite(v)) return;
+  if (v < g_div[k][slot]) g_div[k][slot] = v;
+  if (v > g_div[k][slot + 1]) g_div[k][slot + 1] = v;
+}
+static inline real div_stat(int k, real a, real b) {
+  if (!g_div_init) oracle_div_stats(NULL, 1);
+  const real q = a / b;
+  div_rec(k, a, 0);
+  div_rec(k, b, 2);
+  div_rec(k, q, 4);
+  g_div[k][6] += 1.0;
+  if (a == 0) g_div[k][7] += 1.0;
+  return q;
+}
+#define DV(k, a, b) div_stat((k), (a), (b))
+#else
+#define DV(k, a, b) ((a) / (b))
+#endif
+
 #if defined(ORACLE_DOUBLE)
 #define EXP exp
 #define LOG log
@@ -605,11 +646,11 @@ static void sfcdif1(ctx_t* X, int iter, real SFCTMP, real RHOAIR, real H, real Q
     MOZ2 = K(0.0);
   } else {
     real TVIR = (K(1.0) + K(0.61) * QAIR) * SFCTMP;
-    real TMP1 = KARMAN * (GRAV / TVIR) * H / (RHOAIR * CPAIR);
+    real TMP1 = DV(1, KARMAN * DV(0, GRAV, TVIR) * H, (RHOAIR * CPAIR));
     if (FABS(TMP1) <= MPEl) TMP1 = MPEl;
-    MOL = K(-1.0) * p3(*FV) / TMP1;
-    *MOZ = rmin((ZLVL - ZPD) / MOL, K(1.0));
-    MOZ2 = rmin((K(2.0) + Z0H) / MOL, K(1.0));
+    MOL = DV(2, K(-1.0) * p3(*FV), TMP1);
+    *MOZ = rmin(DV(3, (ZLVL - ZPD), MOL), K(1.0));
+    MOZ2 = rmin(DV(4, (K(2.0) + Z0H), MOL), K(1.0));
   }
   if (MOZOLD * *MOZ < K(0.0)) *MOZSGN = *MOZSGN + 1;
   if (*MOZSGN >= 2) {
@@ -661,8 +702,8 @@ static void sfcdif1(ctx_t* X, int iter, real SFCTMP, real RHOAIR, real H, real Q
   if (FABS(CHFH) <= MPEl) CHFH = MPEl;
   if (FABS(CM2FM2) <= MPEl) CM2FM2 = MPEl;
   if (FABS(CH2FH2) <= MPEl) CH2FH2 = MPEl;
-  *CM = KARMAN * KARMAN / (CMFM * CMFM);
-  *CH = KARMAN * KARMAN / (CMFM * CHFH);
+  *CM = DV(5, KARMAN * KARMAN, (CMFM * CMFM));
+  *CH = DV(6, KARMAN * KARMAN, (CMFM * CHFH));
   *CH2 = KARMAN * KARMAN / (CM2FM2 * CH2FH2);
   *FV = UR * SQRT(*CM);
   *CH2 = KARMAN * *FV / CH2FH2;
@@ -756,10 +797,10 @@ static void ragrb(const nmp_params* P, int iter, real VAI, real RHOAIR, real HG,
   *MOZG = K(0.0);
   real MOLG = K(0.0);
   if (iter > 1) {
-    real TMP1 = KARMAN * (GRAV / TAH) * HG / (RHOAIR * CPAIR);
+    real TMP1 = DV(11, KARMAN * DV(10, GRAV, TAH) * HG, (RHOAIR * CPAIR));
     if (FABS(TMP1) <= MPEl) TMP1 = MPEl;
-    MOLG = K(-1.) * p3(FV) / TMP1;
-    *MOZG = rmin((ZPD - Z0MG) / MOLG, K(1.0));
+    MOLG = DV(12, K(-1.) * p3(FV), TMP1);
+    *MOZG = rmin(DV(13, (ZPD - Z0MG), MOLG), K(1.0));
   }
   real FHGNEW = (*MOZG < K(0.0)) ? POW(K(1.0) - K(15.0) * *MOZG, K(-0.25))
                                   : K(1.0) + K(4.7) * *MOZG;
@@ -768,14 +809,14 @@ static void ragrb(const nmp_params* P, int iter, real VAI, real RHOAIR, real HG,
   else
     *FHG = K(0.5) * (*FHG + FHGNEW);
   real CWPC = SQRT(CWP * VAI * HCAN * *FHG);
-  real TMP1 = EXP(-CWPC * Z0HG / HCAN);
-  real TMP2 = EXP(-CWPC * (Z0H + ZPD) / HCAN);
-  real TMPRAH2 = HCAN * EXP(CWPC) / CWPC * (TMP1 - TMP2);
+  real TMP1 = EXP(DV(14, -CWPC * Z0HG, HCAN));
+  real TMP2 = EXP(DV(15, -CWPC * (Z0H + ZPD), HCAN));
+  real TMPRAH2 = DV(16, HCAN * EXP(CWPC), CWPC) * (TMP1 - TMP2);
   real KH = rmax(KARMAN * FV * (HCAN - ZPD), MPEl);
   *RAMG = K(0.0);
-  *RAHG = TMPRAH2 / KH;
+  *RAHG = DV(17, TMPRAH2, KH);
   *RAWG = *RAHG;
-  real TMPRB = CWPC * K(50.0) / (K(1.0) - EXP(-CWPC / K(2.0)));
+  real TMPRB = DV(18, CWPC * K(50.0), (K(1.0) - EXP(-CWPC / K(2.0))));
   *RB = TMPRB * SQRT(VEGP(dleaf) / UC);
 }
 
@@ -929,7 +970,7 @@ static void vege_flux(ctx_t* X, int ISNOW, int lutyp, real DT, real SAV, real SA
       *CM = *CM / UR;
     }
     RAMC = rmax(K(1.0), K(1.0) / (*CM * UR));
-    RAHC = rmax(K(1.0), K(1.0) / (*CH * UR));
+    RAHC = rmax(K(1.0), DV(7, K(1.0), (*CH * UR)));
     RAWC = RAHC;
     ragrb(P, iter, VAIE, RHOAIR, HG, *TAH, ZPD, Z0MG, Z0HG, HCAN, UC, Z0H, FV, CWP, lutyp, MPEl,
           &MOZG, &FHG, &RAMG, &RAHG, &RAWG, &RB);
@@ -954,43 +995,43 @@ static void vege_flux(ctx_t* X, int ISNOW, int lutyp, real DT, real SAV, real SA
         canres(P, lutyp, SFCPRS, *TV, PARSHA, *EAH, BTRAN, &o->RSSHA, &o->PSNSHA);
       }
     }
-    CAH = K(1.0) / RAHC;
-    CVH = K(2.0) * VAIE / RB;
-    CGH = K(1.0) / RAHG;
+    CAH = DV(20, K(1.0), RAHC);
+    CVH = DV(21, K(2.0) * VAIE, RB);
+    CGH = DV(22, K(1.0), RAHG);
     COND = CAH + CVH + CGH;
-    ATA = (SFCTMP * CAH + *TG * CGH) / COND;
-    BTA = CVH / COND;
+    ATA = DV(23, (SFCTMP * CAH + *TG * CGH), COND);
+    BTA = DV(24, CVH, COND);
     CSH = (K(1.0) - BTA) * RHOAIR * CPAIR * CVH;
-    CAW = K(1.0) / RAWC;
-    CEW = FWET * VAIE / RB;
-    CTW = (K(1.0) - FWET) * (LAISUNE / (RB + o->RSSUN) + LAISHAE / (RB + o->RSSHA));
-    CGW = K(1.0) / (RAWG + RSURF);
+    CAW = DV(25, K(1.0), RAWC);
+    CEW = DV(26, FWET * VAIE, RB);
+    CTW = (K(1.0) - FWET) * (DV(27, LAISUNE, (RB + o->RSSUN)) + DV(28, LAISHAE, (RB + o->RSSHA)));
+    CGW = DV(29, K(1.0), (RAWG + RSURF));
     COND = CAW + CEW + CTW + CGW;
-    AEA = (EAIR * CAW + ESTG * CGW) / COND;
-    BEA = (CEW + CTW) / COND;
-    CEV = (K(1.0) - BEA) * CEW * RHOAIR * CPAIR / GAMMAV;
-    CTR = (K(1.0) - BEA) * CTW * RHOAIR * CPAIR / GAMMAV;
+    AEA = DV(30, (EAIR * CAW + ESTG * CGW), COND);
+    BEA = DV(31, (CEW + CTW), COND);
+    CEV = DV(32, (K(1.0) - BEA) * CEW * RHOAIR * CPAIR, GAMMAV);
+    CTR = DV(33, (K(1.0) - BEA) * CTW * RHOAIR * CPAIR, GAMMAV);
     *TAH = ATA + BTA * *TV;
     *EAH = AEA + BEA * ESTV;
     o->IRC = fveg * (AIR + CIR * p4(*TV));
     o->SHC = fveg * RHOAIR * CPAIR * CVH * (*TV - *TAH);
-    o->EVC = fveg * RHOAIR * CPAIR * CEW * (ESTV - *EAH) / GAMMAV;
-    o->TR = fveg * RHOAIR * CPAIR * CTW * (ESTV - *EAH) / GAMMAV;
+    o->EVC = DV(34, fveg * RHOAIR * CPAIR * CEW * (ESTV - *EAH), GAMMAV);
+    o->TR = DV(35, fveg * RHOAIR * CPAIR * CTW * (ESTV - *EAH), GAMMAV);
     if (*TV > TFRZ)
       o->EVC = rmin(CANLIQ * LATHEAV / DT, o->EVC);
     else
       o->EVC = rmin(CANICE * LATHEAV / DT, o->EVC);
     B = SAV - o->IRC - o->SHC - o->EVC - o->TR;
     A = fveg * (K(4.0) * CIR * p3(*TV) + CSH + (CEV + CTR) * DESTV);
-    DTV = B / A;
+    DTV = DV(36, B, A);
     o->IRC = o->IRC + fveg * K(4.0) * CIR * p3(*TV) * DTV;
     o->SHC = o->SHC + fveg * CSH * DTV;
     o->EVC = o->EVC + fveg * CEV * DESTV * DTV;
     o->TR = o->TR + fveg * CTR * DESTV * DTV;
     *TV = *TV + DTV;
-    H = RHOAIR * CPAIR * (*TAH - SFCTMP) / RAHC;
-    HG = RHOAIR * CPAIR * (*TG - *TAH) / RAHG;
-    *QSFC = (K(0.622) * *EAH) / (SFCPRS - K(0.378) * *EAH);
+    H = DV(37, RHOAIR * CPAIR * (*TAH - SFCTMP), RAHC);
+    HG = DV(38, RHOAIR * CPAIR * (*TG - *TAH), RAHG);
+    *QSFC = DV(39, (K(0.622) * *EAH), (SFCPRS - K(0.378) * *EAH));
     if (LITER == 1) break;
     if (iter >= 5 && FABS(DTV) <= K(0.01) && LITER == 0) LITER = 1;
   }

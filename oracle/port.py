@@ -18,7 +18,8 @@ LIBS = {4: os.path.join(HERE, "build", "liboracle_f32.so"),
         8: os.path.join(HERE, "build", "liboracle_f64.so"),
         "cr": os.path.join(HERE, "build", "liboracle_f32cr.so"),
         "4s": os.path.join(HERE, "build", "liboracle_f32_stats.so"),
-        "8s": os.path.join(HERE, "build", "liboracle_f64_stats.so")}
+        "8s": os.path.join(HERE, "build", "liboracle_f64_stats.so"),
+        "4d": os.path.join(HERE, "build", "liboracle_f32_divstats.so")}
 # trip counts recorded by the stats builds, per column (noahmp_oracle.c ITER_STAT)
 STAT_LOOPS = ("vege_flux Newton", "stomata bisection", "frh2o", "soilwater sub-steps",
               "bare_flux Newton")
@@ -61,6 +62,8 @@ def _lib(precision):
         assert lib.oracle_real_bytes() == (8 if precision in (8, "8s") else 4)
         if precision in ("4s", "8s"):
             lib.oracle_set_stats.argtypes = [C.c_void_p]
+        if precision == "4d":
+            lib.oracle_div_stats.argtypes = [C.c_void_p, C.c_int]
         _libs[precision] = (lib, rt)
     return _libs[precision]
 
@@ -101,6 +104,16 @@ def step_stats(P: dict, options, zsoil, dt, yearlen, julian, state, isnow, stati
     finally:
         lib.oracle_set_stats(None)
     return (*out, buf[:, :len(STAT_LOOPS)].copy())
+
+
+def div_stats(reset: bool = False) -> np.ndarray:
+    """Division operand ranges recorded by the "4d" build since the last reset
+    (noahmp_oracle.c ORACLE_DIV_STATS): (40 sites, 8) = min|a|, max|a|, min|b|,
+    max|b|, min|q|, max|q| over nonzero finite values, calls, zero numerators."""
+    lib, _ = _lib("4d")
+    out = np.zeros((40, 8), np.float64)
+    lib.oracle_div_stats(out.ctypes.data, int(reset))
+    return out
 
 
 def prepare_run(P: dict, options, zsoil, dt, yearlen, julian0, state, isnow, static_f, static_i,

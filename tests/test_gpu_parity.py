@@ -792,6 +792,7 @@ def test_sflx_columns_caller_ficeold_vs_reference(engines):
     ("global", 1_036_800, 2, 8),       # config #5 in fp64 (vs the fp64 restatement)
     ("casenml", 65536, 1, 8),          # config #2: replicated case.nml columns, fp64
     ("conus", 524_288, 1, 4),          # config #4: one of 8 shards of the CONUS-like grid
+    ("conus", 4_194_304, 1, 4),        # config #4 whole: all 4,194,304 columns on one GPU
 ])
 def test_full_size_sample_vs_oracle(engines, oracle_port, kind, ncol, opt_veg, precision):
     """BASELINE sizes: two steps of every column on the GPU, then a seeded
@@ -983,4 +984,45 @@ def test_tiny_canopy_wet_fraction_bit_exact(engines, oracle_port, fwet, variant)
     got, gd = cs.state.cpu().numpy(), diag.cpu().numpy()
     ok = bit_equal(got, est).all(0) & bit_equal(gd, edg).all(0)
     assert ok.all(), f"{(~ok).sum()} columns differ ({int((~ok & hit).sum())} of them pushed)"
+    assert np.array_equal(cs.isnow.cpu().numpy(), eisn)
+
+
+@pytest.mark.parametrize("variant", VARIANTS)
+@pytest.mark.parametrize("perturb", ["wind", "pressure", "fwet", "mixed"])
+def test_canopy_division_domain_fallback_bit_exact(engines, oracle_port, perturb, variant):
+    """The canopy Newton loop divides with the short exact sequence inside the
+    range proof's domain (csrc/vege_domain.h, tools/div_proof.py) and falls
+    back to IEEE division for a lane outside it.  Columns pushed outside the
+    domain -- wind of 150-400 m/s, surface pressure of 2.5e4 Pa, a canopy wet
+    fraction of 1e-20, or all three on different columns -- next to untouched
+    ones: every column equals the C restatement bit for bit, in both
+    occupancy instantiations."""
+    P = __import__("noahmp_amd.params", fromlist=["Params"]).Params.builtin()
+    from noahmp_amd.engine import ColumnState
+    opts = [L.CASE_NML_OPTIONS[k] for k in L.OPTION_NAMES]
+    eng = engines(opts, variant=variant)
+    n = 4096
+    cols = cases.make_columns(n, "mixed", P.as_dict(), seed=31, julian=180.0)
+    f = cases.forcing_step(cols, 180.3, 366, 0, seed=31).copy()
+    st = cols.state.copy()
+    rng = np.random.default_rng(7)
+    hit = np.arange(n) % 3 == 0
+    kinds = {"wind": [0], "pressure": [1], "fwet": [2], "mixed": [0, 1, 2]}[perturb]
+    which = np.where(hit, rng.choice(kinds, n), -1)
+    fi = L.FORCING.index
+    f[fi("UU"), which == 0] = rng.uniform(150.0, 400.0, (which == 0).sum()).astype(np.float32)
+    f[fi("SFCPRS"), which == 1] = np.float32(2.5e4)
+    f[fi("PSFC"), which == 1] = np.float32(2.5e4)
+    st[L.s("FWET").start, which == 2] = np.float32(1e-20)
+    cols = dataclasses.replace(cols, state=st)
+    cs = ColumnState.from_host(cols, DEV)
+    diag = torch.zeros((L.NDIAG_FULL, n), device=DEV)
+    eng.step(cs, torch.as_tensor(f, device=DEV), cases.CASE_NML_ZSOIL, 1800.0, 180.3, 366, diag,
+             L.DIAG_FULL_LEVEL)
+    torch.cuda.synchronize()
+    est, eisn, edg, _ = oracle_port.step(load_params(), tuple(opts), cases.CASE_NML_ZSOIL, 1800.0,
+                                         366, 180.3, st, cols.isnow, cols.static_f, cols.static_i, f)
+    got, gd = cs.state.cpu().numpy(), diag.cpu().numpy()
+    ok = bit_equal(got, est).all(0) & bit_equal(gd, edg).all(0)
+    assert ok.all(), f"{(~ok).sum()} columns differ ({int((~ok & hit).sum())} of them perturbed)"
     assert np.array_equal(cs.isnow.cpu().numpy(), eisn)

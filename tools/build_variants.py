@@ -74,6 +74,17 @@ VARIANTS = {
     "ldswait0": {"f32": ["-DNMP_LDS_EXPLICIT_WAIT=0"]},
     "dgetbr": ("-DNMP_DGET_BRANCHY",),
     "fdiv7": {"f32": ["-DNMP_F32_DIV=7"]},
+    # round 4: the canopy loop with IEEE division only (before the range-proved
+    # short division became the default)
+    "vd0": {"f32": ["-DNMP_VEGE_DIV=0"]},
+    # the default build plus a device counter of lanes that re-ran the canopy
+    # loop with IEEE division (nmp_debug_fallback_count)
+    "fbcount": {"f32": ["-DNMP_COUNT_FALLBACK"]},
+    # timing probes of the range-checked canopy division (not exact in general)
+    "vdnodom": {"f32": ["-DNMP_VD_NODOMAIN"]},
+    "vdnowin": {"f32": ["-DNMP_VD_NOWIN"]},
+    "vdallfast": {"f32": ["-DNMP_VD_ALLFAST"]},
+    "vdnone": {"f32": ["-DNMP_VD_NODOMAIN", "-DNMP_VD_NOWIN", "-DNMP_VD_ALLFAST"]},
     "nopeel": ("-DNMP_VEGE_NOPEEL",),
     "vu2": ("-DNMP_VEGE_UNROLL=2",),
     "vu3": ("-DNMP_VEGE_UNROLL=3",),

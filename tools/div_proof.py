@@ -1,0 +1,266 @@
+"""Range proof of the canopy Newton loop's short divisions (DivFast32).
+
+DivFast32 (csrc/sflx_math.h) returns IEEE a/b bit for bit when
+  b is normal with a normal reciprocal: |b| in [2^-126, 2^126],
+  the fma residual a - b*q is not subnormal: a = 0 or |a| >= 2^-102,
+  the quotient is normal: a = 0 or |a/b| in [2^-126, 2^126],
+or when an operand is zero, infinite or NaN (v_div_fixup_f32 takes over).
+The first three hold on every pair of significands at every scale
+(tools/fdiv_exhaust.hip, profiles/r03/fdiv_exhaust2.txt).
+
+This script derives, for every division the loop runs with DivFast32, a
+bound on |a|, |b| and |a/b| from the input domain of csrc/vege_domain.h (the
+kernel checks it per column and falls back to IEEE division outside it), in
+the loop's own order (sflx_kernel.hip vege_flux; func.f90:2744-2877 with
+sfcdif1 :3353-3508 and ragrb :3260-3350), and checks each against that
+region.  Magnitudes are intervals [lo, hi] of |x| for nonzero x plus a flag
+for "x may be 0".  Every bound is widened by 2^-20 per operation, more than
+the kernel's rounding (2^-24 per operation, a few ulps per libm call).
+
+Differences of floats are bounded below by granularity: x - y (x, y floats)
+is 0 or at least 2^(E - 23), E the smaller binary exponent of x and y,
+because both are multiples of that power of two; rounding keeps it.
+
+Loop-carried values are bounded by induction over the iterations: the values
+an iteration starts from (TV, TAH, H, HG, FV, FHG, MOZ/FM/FH) are assumed in
+the intervals below, the iteration is shown to end inside them again; TV and
+RAHG are the two the kernel checks at run time, every iteration.
+
+    python tools/div_proof.py            # prints the per-site table, exit 1 on a failure
+"""
+import math
+import os
+import re
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HDR = os.path.join(ROOT, "noahmp-1_amd", "csrc", "vege_domain.h")
+
+W = 2.0 ** -20            # widening per operation
+A_MIN = 2.0 ** -102       # smallest nonzero numerator
+N_MIN, N_MAX = 2.0 ** -126, 2.0 ** 126
+KARMAN, GRAV, CPAIR, SB = 0.4, 9.80616, 1004.64, 5.67e-08
+HVAP, HSUB, TFRZ = 2.51e6, 2.8440e6, 273.16
+
+
+def domain():
+    d = {}
+    for m in re.finditer(r"#define (NMP_DOM_\w+) ([-+0-9.eE]+)", open(HDR).read()):
+        d[m.group(1)[8:]] = float(m.group(2))
+    return d
+
+
+class M:
+    """|x| in [lo, hi] for x != 0; z: x may be 0."""
+
+    def __init__(self, lo, hi, z=False):
+        assert 0 < lo <= hi, (lo, hi)
+        self.lo, self.hi, self.z = lo * (1 - W), hi * (1 + W), z
+
+    def __mul__(self, o):
+        o = o if isinstance(o, M) else M(abs(o), abs(o))
+        return M(self.lo * o.lo, self.hi * o.hi, self.z or o.z)
+
+    __rmul__ = __mul__
+
+    def __add__(self, o):   # terms of one sign (all >= 0 here)
+        lo = min(self.lo, o.lo) if (self.z or o.z) else max(self.lo, o.lo)
+        return M(lo, self.hi + o.hi, self.z and o.z)
+
+    def nz(self):           # the same magnitudes, known nonzero
+        return M(self.lo, self.hi)
+
+    def __repr__(self):
+        return f"{'0|' if self.z else ''}[{self.lo:.3g}, {self.hi:.3g}]"
+
+
+def c(v):
+    return M(abs(v), abs(v))
+
+
+def diff(x, y):
+    """|x - y| for floats x, y with |x| <= x.hi etc.: 0 or >= 2^(E-23)."""
+    e = math.floor(math.log2(min(x.lo, y.lo)))
+    return M(2.0 ** (e - 23), x.hi + y.hi, True)
+
+
+def fn(f, x):            # monotone increasing f on magnitudes
+    return M(f(x.lo), f(x.hi), x.z)
+
+
+rows, bad = [], []
+
+
+def site(name, a, b, ref, note=""):
+    """Record one division a/b; returns the quotient's magnitude interval."""
+    q = M(a.lo / b.hi, a.hi / b.lo, a.z)
+    ok = (not b.z and N_MIN <= b.lo and b.hi <= N_MAX and A_MIN <= a.lo
+          and N_MIN <= q.lo and q.hi <= N_MAX)
+    rows.append((name, ref, a, b, q, ok, note))
+    if not ok:
+        bad.append(name)
+    return q
+
+
+def esat_range():
+    def poly(t, cs):
+        v = 0.0
+        for k in reversed(cs):
+            v = v * t + k
+        return 100.0 * v
+    w = [6.107799961, 4.436518521E-01, 1.428945805E-02, 2.650648471E-04, 3.031240396E-06,
+         2.034080948E-08, 6.136820929E-11]
+    i = [6.109177956, 5.034698970E-01, 1.886013408E-02, 4.176223716E-04, 5.824720280E-06,
+         4.838803174E-08, 1.838826904E-10]
+    dw = [4.438099984E-01, 2.857002636E-02, 7.938054040E-04, 1.215215065E-05, 1.036561403E-07,
+          3.532421810e-10, -7.090244804E-13]
+    di = [5.030305237E-01, 3.773255020E-02, 1.267995369E-03, 2.477563108E-05, 3.005693132E-07,
+          2.158542548E-09, 7.131097725E-12]
+    ts = [k / 100.0 for k in range(-5000, 5001)]   # tdc clamps to [-50, 50] C
+    es = [poly(t, w if t > 0 else i) for t in ts]
+    des = [poly(t, dw if t > 0 else di) for t in ts]
+    return M(min(es), max(es)), M(min(des), max(des))
+
+
+def main():
+    D = domain()
+    # ---- loop-invariant inputs: the kernel's entry check (vege_domain.h) ----
+    T = M(D["T_LO"], D["T_HI"])                    # SFCTMP, TG; TV (every iteration)
+    rho = M(D["RHO_LO"], D["RHO_HI"])
+    rhocp = rho * CPAIR
+    qair = M(1e-30, 1.0, True)                     # checked 0 <= QAIR <= 1
+    tvir = M(T.lo, T.hi * 1.61)                    # (1 + 0.61 QAIR) SFCTMP
+    ur = M(1.0, D["UR_HI"])
+    tmpc = M(D["TMPC_LO"], D["TMPC_HI"])           # TMPCM = TMPCH, TMPCM2 = TMPCH2
+    dz = M(D["DZ_LO"], D["DZ_HI"])                 # ZLVL - ZPD
+    z0 = M(D["Z0_LO"], D["Z0_HI"])                 # Z0M = Z0H, Z0MG
+    d2 = M(2.0, 2.0 + D["Z0_HI"])                  # 2 + Z0H
+    hcan = M(D["HCAN_LO"], D["HCAN_HI"])
+    zpd = M(D["Z0_LO"], D["HCAN_HI"], True)        # 0 or >= Z0_LO, <= HCAN
+    cwph = M(D["CWPH_LO"], D["CWPH_HI"])           # CWP * VAIE * HCAN
+    vaie = M(D["VAI_LO"], 6.0)
+    lai = M(D["LAI_LO"], 6.0, True)
+    fwet = M(D["FWET_LO"], 1.0, True)
+    fveg = M(D["FVEG_LO"], 1.0)
+    sdl = M(D["SDL_LO"], D["SDL_HI"])              # SQRT(DLEAF/UC)
+    rsurf_hi = D["RSURF_HI"]
+    p = M(D["P_LO"], D["P_HI"])
+    eair_hi = D["EAIR_HI"]
+    gammav = M(CPAIR * p.lo / (0.622 * HSUB), CPAIR * p.hi / (0.622 * HVAP))
+    es, des = esat_range()                          # ESTG, ESTV and DESTV
+    rs_hi = D["RS_HI"]
+    rahg_w = M(D["RAHG_LO"], D["RAHG_HI"])          # checked every iteration
+    tah = M(T.lo * (1 - 1e-5), T.hi * (1 + 1e-5))   # convex combination of SFCTMP, TG, TV
+    dT = diff(T, tah)                               # TAH - SFCTMP, TG - TAH, TV - TAH
+
+    # ---- loop-carried values an iteration starts from (induction hypothesis) ----
+    cmfm = M(0.1 * tmpc.lo, tmpc.hi + 5.0)          # TMPCM - FM, FM in [-5, 0.9 TMPCM]
+    cm = M(0.16 / cmfm.hi ** 2, 0.16 / cmfm.lo ** 2)
+    fv = ur * fn(math.sqrt, cm)                     # FV = UR * SQRT(CM)
+    rahc = M(1.0, 1.0 / (cm.lo * ur.lo))            # MAX(1, 1/(CH*UR))
+    h = M((rhocp * dT).lo / rahc.hi, (rhocp * dT).hi, True)
+    hg = M((rhocp * dT).lo / rahg_w.hi, (rhocp * dT).hi / rahg_w.lo, True)
+    fhg_lo = None                                   # derived below, then checked
+
+    # ---- sfcdif1 (iter >= 2), :3405-3441, sflx_kernel.hip sfcdif1 ----
+    kgtv = KARMAN * site("GRAV / TVIR", c(GRAV), tvir, ":3430 (once per loop)")
+    tmp1 = site("TMP1 = KGTV*H / RHOCP", kgtv * h, rhocp, ":3431")
+    tmp1 = M(1e-6, tmp1.hi)                         # IF (ABS(TMP1) <= MPE) TMP1 = MPE
+    fv3 = fn(lambda x: x ** 3, fv)
+    mol = site("MOL = -FV**3 / TMP1", fv3, tmp1, ":3433")
+    site("MOZ = (ZLVL-ZPD) / MOL", dz, mol, ":3434", "then MIN(., 1)")
+    site("MOZ2 = (2+Z0H) / MOL", d2, mol, ":3435", "then MIN(., 1)")
+    cm_q = site("CM = KARMAN**2 / CMFM**2", c(0.16), cmfm * cmfm, ":3499",
+                "CMFM >= 0.1 TMPCM: FM <= 0.9 TMPCM (:3455)")
+    site("CH = KARMAN**2 / (CMFM*CHFH)", c(0.16), cmfm * cmfm, ":3500")
+    assert cm_q.lo >= cm.lo * (1 - 1e-4) and cm_q.hi <= cm.hi * (1 + 1e-4)
+    # ---- vege_flux: canopy resistance, :2775 ----
+    site("RAHC: 1 / (CH*UR)", c(1.0), cm * ur, ":2775", "then MAX(1, .)")
+    # ---- ragrb (iter >= 2), :3301-3306 ----
+    gt = site("GRAV / TAH", c(GRAV), tah, ":3313")
+    tmp1g = site("TMP1 = KARMAN*(GRAV/TAH)*HG / RHOCP", KARMAN * gt * hg, rhocp, ":3313")
+    tmp1g = M(1e-6, tmp1g.hi)
+    molg = site("MOLG = -FV**3 / TMP1", fv3, tmp1g, ":3315")
+    dzg = diff(zpd.nz(), z0)                        # ZPD - Z0MG, nonzero >= granularity
+    dzg = M(dzg.lo, D["HCAN_HI"] + D["Z0_HI"], True)
+    mozg = site("MOZG = (ZPD-Z0MG) / MOLG", dzg, molg, ":3316", "then MIN(., 1)")
+    fhg_lo = (1.0 + 15.0 * mozg.hi) ** -0.25        # (1 - 15 MOZG)**-0.25, MOZG < 0
+    fhg = M(fhg_lo, 5.7)                            # 1 + 4.7 MOZG <= 5.7; averages stay inside
+    cwpc = fn(math.sqrt, cwph * fhg)                # SQRT(CWP*VAI*HCAN*FHG)
+    a14 = cwpc * z0
+    q14 = site("CWPC*Z0HG / HCAN", a14, hcan, ":3334", "Z0MG <= HCAN checked: <= CWPC")
+    q14 = M(q14.lo, cwpc.hi)
+    q15 = site("CWPC*(Z0H+ZPD) / HCAN", cwpc * z0, hcan, ":3335",
+               "Z0M + ZPD <= 2 HCAN checked: <= 2 CWPC")
+    q15 = M(q15.lo, 2 * cwpc.hi)
+    tmp1e = M(math.exp(-q14.hi), 1.0)
+    tmp2e = M(math.exp(-q15.hi), 1.0)
+    rah2a = site("HCAN*EXP(CWPC) / CWPC", hcan * fn(math.exp, cwpc), cwpc, ":3336")
+    # TMP1 >= TMP2 (Z0MG <= Z0M + ZPD checked); their difference is 0 or >= granularity
+    dtmp = M(2.0 ** (math.floor(math.log2(tmp2e.lo)) - 23), 1.0, True)
+    kh = M(1e-6, KARMAN * fv.hi * D["HCAN_HI"])    # MAX(KARMAN*FV*(HCAN-ZPD), MPE)
+    site("RAHG = TMPRAH2 / KH", rah2a * dtmp, kh, ":3341", "then checked in [RAHG_LO, RAHG_HI]")
+    den_rb = M(-math.expm1(-cwpc.lo / 2) * 0.999, -math.expm1(-cwpc.hi / 2))
+    site("TMPRB = CWPC*50 / (1-EXP(-CWPC/2))", 50 * cwpc, den_rb, ":3346")
+    # 50x / (1 - exp(-x/2)) increases with x, from 100 at x -> 0
+    tmprb = M(99.0, 50 * cwpc.hi / -math.expm1(-cwpc.hi / 2) * 1.001)
+    rb = tmprb * sdl
+    rahg = rahg_w
+    # ---- vege_flux body, :2808-2870 ----
+    cah = site("CAH = 1 / RAHC", c(1.0), rahc, ":2817")
+    cvh = site("CVH = 2*VAIE / RB", 2 * vaie, rb, ":2818")
+    cgh = site("CGH = 1 / RAHG", c(1.0), rahg, ":2819")
+    cond = cah + cvh + cgh
+    site("ATA = (SFCTMP*CAH + TG*CGH) / COND", T * cah + T * cgh, cond, ":2821")
+    site("BTA = CVH / COND", cvh, cond, ":2822")
+    site("CAW = 1 / RAWC", c(1.0), rahc, ":2826")
+    cew = site("CEW = FWET*VAIE / RB", fwet * vaie, rb, ":2827")
+    rbrs = M(rb.lo, rb.hi + rs_hi)
+    t1 = site("LAISUNE / (RB+RSSUN)", lai, rbrs, ":2828", "RSSUN, RSSHA <= RS_HI checked")
+    site("LAISHAE / (RB+RSSHA)", lai, rbrs, ":2828")
+    # CTW = (1-FWET)*(...): its bound matters only through BEA's numerator
+    # CEW + CTW, which is CTW = the two terms when FWET = 0 and >= CEW otherwise
+    ctw = M(t1.lo, 2 * t1.hi, True)
+    cgw = site("CGW = 1 / (RAWG+RSURF)", c(1.0), M(rahg.lo, rahg.hi + rsurf_hi), ":2829")
+    cond2 = cah + cew + ctw + cgw
+    site("AEA = (EAIR*CAW + ESTG*CGW) / COND", M(es.lo * cgw.lo, eair_hi + es.hi * cgw.hi), cond2,
+         ":2831")
+    bea = site("BEA = (CEW+CTW) / COND", M(min(cew.lo, ctw.lo), cew.hi + ctw.hi, True), cond2,
+               ":2832", "FWET = 0: CTW = the LAI terms; FWET > 0: >= CEW")
+    one_m_bea = M(2.0 ** -24, 1.0, True)            # BEA <= 1; 1 - BEA is 0 or >= 2^-24
+    site("CEV = (1-BEA)*CEW*RHOAIR*CPAIR / GAMMAV", one_m_bea * cew * rhocp, gammav, ":2833")
+    # EAH = AEA + BEA*ESTV lies between 0 and max(EAIR, ESTG, ESTV); ESTV >= es.lo, so
+    # ESTV - EAH is 0 or >= 2^(E - 23) with E the exponent of es.lo / 2
+    de = M(2.0 ** (math.floor(math.log2(es.lo / 2)) - 23), max(es.hi, eair_hi), True)
+    site("EVC = FVEG*RHOAIR*CPAIR*CEW*(ESTV-EAH) / GAMMAV", fveg * rhocp * cew * de, gammav,
+         ":2842")
+    eah = M(es.lo * cgw.lo / cond2.hi, max(es.hi, eair_hi))
+    h_q = site("H = RHOAIR*CPAIR*(TAH-SFCTMP) / RAHC", rhocp * dT, rahc, ":2864")
+    hg_q = site("HG = RHOAIR*CPAIR*(TG-TAH) / RAHG", rhocp * dT, rahg, ":2865")
+    site("QSFC = 0.622*EAH / (SFCPRS-0.378*EAH)", 0.622 * eah,
+         M(p.lo - 0.378 * eah.hi, p.hi), ":2868")
+    # ---- induction: the iteration ends inside the intervals it started from ----
+    assert h_q.hi <= h.hi * 1.001 and h_q.lo >= h.lo * 0.999, (h_q, h)
+    assert hg_q.hi <= hg.hi * 1.001 and hg_q.lo >= hg.lo * 0.999, (hg_q, hg)
+    assert eah.hi <= max(es.hi, eair_hi) * 1.001
+    assert p.lo - 0.378 * eah.hi > 0
+
+    print(f"domain: {HDR}")
+    print(f"exact region: |b| in [2^-126, 2^126], a = 0 or |a| >= 2^-102, |a/b| in [2^-126, 2^126]")
+    print(f"{'site':46s} {'func.f90':8s} {'|a|':>22s} {'|b|':>22s} {'|a/b|':>22s}  ok")
+    for name, ref, a, b, q, ok, note in rows:
+        print(f"{name:46s} {ref:8s} {a!r:>22s} {b!r:>22s} {q!r:>22s}  {'yes' if ok else 'NO'}"
+              + (f"  ({note})" if note else ""))
+    print("IEEE kept (not in the table): CTR :2834, TR :2843, DTV = B/A :2852 -- their numerators "
+          "are products of up to four small factors whose bound falls below 2^-102")
+    print(f"derived: FHG >= {fhg_lo:.3g}, CWPC in {cwpc!r}, FV in {fv!r}, RAHC in {rahc!r}, "
+          f"RB in {rb!r}")
+    if bad:
+        print("FAILED:", bad)
+        return 1
+    print(f"all {len(rows)} sites inside the exact region")
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())
