@@ -942,6 +942,10 @@ static __device__ unsigned int nmp_fb_reason[32];
 #ifndef NMP_VEGE_DIV
 #define NMP_VEGE_DIV 1
 #endif
+// NMP_BARE_DIV: the same for the bare-ground Newton loop (bare_flux)
+#ifndef NMP_BARE_DIV
+#define NMP_BARE_DIV 1
+#endif
 #ifndef NMP_VEGE_UNROLL
 #define NMP_VEGE_UNROLL 1
 #endif
@@ -1317,6 +1321,18 @@ DEV void sflx_column(const DevParams& P, const KArgs<T>& A, Col<T>& c, const Sin
   c.ch = out.ls(NMP_S_CH); c.tbot = out.lf(NMP_F_TBOT); c.foln = out.lf(NMP_F_FOLN);
   c.co2air = out.la(NMP_A_CO2AIR); c.o2air = out.la(NMP_A_O2AIR);
   NMP_PHASE(4);
+#ifdef NMP_COUNT_FALLBACK
+  // (probe builds) which condition sent the lane to an IEEE loop
+  unsigned fb_why = 0;
+#define NMP_DOM(flag, bit, cond)                 \
+  do {                                           \
+    const bool c_ = (cond);                      \
+    flag = flag & c_;                            \
+    if (!c_) fb_why |= 1u << (bit);              \
+  } while (0)
+#else
+#define NMP_DOM(flag, bit, cond) flag = flag & (cond)
+#endif
   // ---- vege_flux: func.f90:2465-2964 ----
   T tgv = L(0.0), cmv = L(0.0);
   int vtrips = 0;
@@ -1350,18 +1366,6 @@ DEV void sflx_column(const DevParams& P, const KArgs<T>& A, Col<T>& c, const Sin
     // The loop-invariant half of the range proof's domain (vege_domain.h,
     // tools/div_proof.py), evaluated once per column before the loop; NaN
     // fails every comparison.
-#ifdef NMP_COUNT_FALLBACK
-    // (probe builds) which condition sent the lane to the IEEE loop
-    unsigned fb_why = 0;
-#define NMP_DOM(flag, bit, cond)                 \
-  do {                                           \
-    const bool c_ = (cond);                      \
-    flag = flag & c_;                            \
-    if (!c_) fb_why |= 1u << (bit);              \
-  } while (0)
-#else
-#define NMP_DOM(flag, bit, cond) flag = flag & (cond)
-#endif
     auto vege_domain_ok = [&]() -> bool {
       auto in = [](T x, double lo, double hi) { return x >= (T)lo && x <= (T)hi; };
       auto zero_or = [&](T x, double lo, double hi) { return x == L(0.0) || in(x, lo, hi); };
@@ -1594,64 +1598,116 @@ NMP_UNROLL(NMP_LOOP2_UNROLL)
 
   NMP_PHASE(5);
   // ---- bare_flux: func.f90:2967-3257 ----
-  constexpr int kBareUnroll = NMP_BARE_UNROLL;
   T tgb = c.tg, cmb = c.cm, chb = c.ch;
   T irb, shb, evb, ghb, t2mb = L(0.0), q2b = L(0.0), chb2 = L(0.0);
   {
     const T mpe = L(1.0E-6);
-    int mozsgn = 0;
-    T h = L(0.0), fv = L(0.1), moz = L(0.0), fm = L(0.0), fh = L(0.0), fm2 = L(0.0), fh2 = L(0.0);
-    T wstar = L(0.0);
+    int mozsgn;
+    T h, fv, moz, fm, fh, fm2, fh2, wstar;
     T cir = emg * SB;
     T cgh = L(2.0) * df_top / dz_top;
-    T z0h = z0mg, ehb = L(0.0), csh = L(0.0), cev = L(0.0), estg = L(0.0);
+    T z0h = z0mg, ehb, csh, cev, estg;
     // saturation pressure at TGB: each iteration's closing value is the next
     // iteration's opening value (same TGB), so it is carried, not recomputed
     T es_tgb, des_tgb;
-    esat_sel(tdc(tgb), es_tgb, des_tgb);
-    irb = shb = evb = ghb = L(0.0);
     const Sfc1Logs<T, R> lgb = (o.sfc == 1) ? Sfc1Logs<T, R>(zlvl, zpdg, z0mg, z0h, c.status)
                                             : Sfc1Logs<T, R>{};
-    DivRef<T> drb;  // bare_flux keeps the reference's divisions
-    const Sfc1Inv<T> invb = sfc1_inv(drb, c.sfctmp, qair, rhoair, zlvl, zpdg, z0h);
-NMP_UNROLL(kBareUnroll)
-    for (int iter = 1; iter <= 5; ++iter) {
-      if (o.sfc == 1)
-        sfcdif1<T, R>(drb, invb, iter, h, lgb, ur, mpe, moz, mozsgn, fm, fh, fm2, fh2, cmb, chb, fv);
-      if (o.sfc == 2) {
-        sfcdif2<T, R>(iter, z0mg, tgb, thair, ur, (T)P.g.czil, zlvl, cmb, chb, moz, wstar, fv);
-        chb = chb / ur;
-        cmb = cmb / ur;
-        if (c.snowh > L(0.0)) {
-          cmb = rmin(L(0.01), cmb);
-          chb = rmin(L(0.01), chb);
-        }
-      }
-      T rahb = rmax(L(1.0), dv(L(1.0), chb * ur));
-      T rawb = rahb;
-      ehb = dv(L(1.0), rahb);
-      estg = es_tgb;
-      const T destg = des_tgb;
-      csh = dv(rhoair * CPAIR, rahb);
-      cev = dv(dv(rhoair * CPAIR, gammag), rsurf + rawb);
-      irb = cir * p4(tgb) - emg * c.lwdn;
-      shb = csh * (tgb - c.sfctmp);
-      evb = cev * (estg * rhsur - eair);
-      ghb = cgh * (tgb - stc_top);
-      T b = sag - irb - shb - evb - ghb;
-      T a = L(4.0) * cir * p3(tgb) + csh + cev * destg + cgh;
-      T dtg = dv(b, a);
-      irb = irb + L(4.0) * cir * p3(tgb) * dtg;
-      shb = shb + csh * dtg;
-      evb = evb + cev * destg * dtg;
-      ghb = ghb + cgh * dtg;
-      tgb = tgb + dtg;
-      h = csh * (tgb - c.sfctmp);
+    // The bare-ground Newton loop (func.f90:3120-3200) with the division
+    // policy `d`, as the canopy loop: every loop variable starts here, so a
+    // lane outside the range proof's domain can run it again with IEEE
+    // division.  DTG = B/A keeps IEEE division under every policy.
+    auto bare_loop = [&](auto& d) -> bool {
+      constexpr bool kFast = !std::is_same<std::decay_t<decltype(d)>, DivRef<T>>::value;
+      const DivRef<T> dref;
+      bool ok = true;
+      auto in = [](T x, T lo, T hi) { return x >= lo && x <= hi; };
+      tgb = c.tg;
+      cmb = c.cm;
+      chb = c.ch;
+      mozsgn = 0;
+      h = L(0.0); fv = L(0.1); moz = L(0.0); fm = L(0.0); fh = L(0.0); fm2 = L(0.0); fh2 = L(0.0);
+      wstar = L(0.0);
+      ehb = csh = cev = estg = L(0.0);
       esat_sel(tdc(tgb), es_tgb, des_tgb);
-      estg = es_tgb;
-      // QSFC is overwritten every iteration and read only after the loop
-      if (iter == 5) c.qsfc = L(0.622) * (estg * rhsur) / (c.psfc - L(0.378) * (estg * rhsur));
+      irb = shb = evb = ghb = L(0.0);
+      const Sfc1Inv<T> invb = sfc1_inv(d, c.sfctmp, qair, rhoair, zlvl, zpdg, z0h);
+NMP_UNROLL(NMP_BARE_UNROLL)
+      for (int iter = 1; iter <= 5; ++iter) {
+        if constexpr (kFast) NMP_DOM(ok, 20, in(tgb, (T)NMP_DOM_T_LO, (T)NMP_DOM_T_HI));
+        if (o.sfc == 1)
+          sfcdif1<T, R>(d, invb, iter, h, lgb, ur, mpe, moz, mozsgn, fm, fh, fm2, fh2, cmb, chb, fv);
+        if (o.sfc == 2) {
+          sfcdif2<T, R>(iter, z0mg, tgb, thair, ur, (T)P.g.czil, zlvl, cmb, chb, moz, wstar, fv);
+          chb = chb / ur;
+          cmb = cmb / ur;
+          if (c.snowh > L(0.0)) {
+            cmb = rmin(L(0.01), cmb);
+            chb = rmin(L(0.01), chb);
+          }
+        }
+        T rahb = rmax(L(1.0), d.divk(L(1.0), d.rec(chb * ur)));
+        const Recip<T> rrahb = d.rec(rahb);  // RAWB = RAHB
+        ehb = d.divk(L(1.0), rrahb);
+        estg = es_tgb;
+        const T destg = des_tgb;
+        csh = d.div(rhoair * CPAIR, rrahb);
+        cev = d.div(d.div(rhoair * CPAIR, d.rec(gammag)), d.rec(rsurf + rahb));
+        irb = cir * p4(tgb) - emg * c.lwdn;
+        shb = csh * (tgb - c.sfctmp);
+        evb = cev * (estg * rhsur - eair);
+        ghb = cgh * (tgb - stc_top);
+        T b = sag - irb - shb - evb - ghb;
+        T a = L(4.0) * cir * p3(tgb) + csh + cev * destg + cgh;
+        T dtg = dref.div(b, dref.rec(a));
+        irb = irb + L(4.0) * cir * p3(tgb) * dtg;
+        shb = shb + csh * dtg;
+        evb = evb + cev * destg * dtg;
+        ghb = ghb + cgh * dtg;
+        tgb = tgb + dtg;
+        h = csh * (tgb - c.sfctmp);
+        esat_sel(tdc(tgb), es_tgb, des_tgb);
+        estg = es_tgb;
+        // QSFC is overwritten every iteration and read only after the loop
+        if (iter == 5) c.qsfc = L(0.622) * (estg * rhsur) / (c.psfc - L(0.378) * (estg * rhsur));
+      }
+      return ok;
+    };
+    // the loop-invariant half of the bare loop's domain (vege_domain.h)
+    auto bare_domain_ok = [&]() -> bool {
+      auto in = [](T x, double lo, double hi) { return x >= (T)lo && x <= (T)hi; };
+      bool k = true;
+      NMP_DOM(k, 21, in(c.sfctmp, NMP_DOM_T_LO, NMP_DOM_T_HI) & in(qair, 0.0, 1.0) &
+                         in(rhoair, NMP_DOM_RHO_LO, NMP_DOM_RHO_HI) &
+                         in(c.sfcprs, NMP_DOM_P_LO, NMP_DOM_P_HI) & in(ur, 1.0, NMP_DOM_UR_HI));
+      NMP_DOM(k, 22, in(lgb.tmpcm, NMP_DOM_TMPC_LO, NMP_DOM_TMPC_HI) &
+                         in(lgb.tmpch, NMP_DOM_TMPC_LO, NMP_DOM_TMPC_HI) &
+                         in(lgb.tmpcm2, NMP_DOM_TMPC_LO, NMP_DOM_TMPC_HI) &
+                         in(lgb.tmpch2, NMP_DOM_TMPC_LO, NMP_DOM_TMPC_HI));
+      NMP_DOM(k, 23, in(zlvl - zpdg, NMP_DOM_DZ_LO, NMP_DOM_DZ_HI) &
+                         in(z0mg, NMP_DOM_Z0_LO, NMP_DOM_Z0_HI) & in(rsurf, 0.0, NMP_DOM_RSURF_HI));
+#ifdef NMP_VD_NODOMAIN
+      k = true;
+#endif
+      return k;
+    };
+    DivRef<T> drb;
+#if NMP_VEGE_DIV && NMP_BARE_DIV
+    if constexpr (sizeof(T) == 4 && R && OS != 0) {
+      DivFast32 dfb;
+      if (!(bare_domain_ok() & bare_loop(dfb))) {
+#ifdef NMP_COUNT_FALLBACK
+        atomicAdd(&nmp_fallback_ctr, 1u);
+        for (int b = 20; b < 24; ++b)
+          if (fb_why & (1u << b)) atomicAdd(&nmp_fb_reason[b], 1u);
+#endif
+        bare_loop(drb);
+      }
+    } else {
+      bare_loop(drb);
     }
+#else
+    bare_loop(drb);
+#endif
     if (o.stc == 1 && c.snowh > L(0.05) && tgb > TFRZ) {
       tgb = TFRZ;
       irb = cir * p4(tgb) - emg * c.lwdn;

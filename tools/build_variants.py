@@ -77,6 +77,7 @@ VARIANTS = {
     # round 4: the canopy loop with IEEE division only (before the range-proved
     # short division became the default)
     "vd0": {"f32": ["-DNMP_VEGE_DIV=0"]},
+    "bare0": {"f32": ["-DNMP_BARE_DIV=0"]},
     # the default build plus a device counter of lanes that re-ran the canopy
     # loop with IEEE division (nmp_debug_fallback_count)
     "fbcount": {"f32": ["-DNMP_COUNT_FALLBACK"]},

@@ -239,6 +239,22 @@ def main():
     hg_q = site("HG = RHOAIR*CPAIR*(TG-TAH) / RAHG", rhocp * dT, rahg, ":2865")
     site("QSFC = 0.622*EAH / (SFCPRS-0.378*EAH)", 0.622 * eah,
          M(p.lo - 0.378 * eah.hi, p.hi), ":2868")
+    # ---- bare_flux's Newton loop (:3120-3200; sflx_kernel.hip bare_loop) ----
+    # Same sfcdif1 sites with Z0H = Z0MG and ZPD = ZPDG (the snow depth): the
+    # kernel checks the same limits on TMPCM.., ZLVL-ZPDG, Z0MG, SFCTMP, air,
+    # pressure and wind, and TGB at the start of every iteration.  Its H is
+    # CSH*(TGB-SFCTMP) with CSH = RHOAIR*CPAIR/RAHB, RAHB in RAHC's interval, so
+    # H has the canopy loop's interval and every sfcdif1 bound above carries over.
+    rahb = rahc
+    hb = M((rhocp * dT).lo / rahb.hi, (rhocp * dT).hi, True)
+    assert hb.lo >= h.lo * 0.999 and hb.hi <= h.hi * 1.001
+    site("bare: RAHB: 1 / (CH*UR)", c(1.0), cm * ur, ":3167", "then MAX(1, .)")
+    site("bare: EHB = 1 / RAHB", c(1.0), rahb, ":3172")
+    site("bare: CSH = RHOAIR*CPAIR / RAHB", rhocp, rahb, ":3186")
+    gammag = gammav                                  # same formula with LATHEAG
+    cevi = site("bare: RHOAIR*CPAIR / GAMMA", rhocp, gammag, ":3187")
+    site("bare: CEV = (...) / (RSURF+RAWB)", cevi, M(rahb.lo, rahb.hi + rsurf_hi), ":3187")
+
     # ---- induction: the iteration ends inside the intervals it started from ----
     assert h_q.hi <= h.hi * 1.001 and h_q.lo >= h.lo * 0.999, (h_q, h)
     assert hg_q.hi <= hg.hi * 1.001 and hg_q.lo >= hg.lo * 0.999, (hg_q, hg)
@@ -251,8 +267,9 @@ def main():
     for name, ref, a, b, q, ok, note in rows:
         print(f"{name:46s} {ref:8s} {a!r:>22s} {b!r:>22s} {q!r:>22s}  {'yes' if ok else 'NO'}"
               + (f"  ({note})" if note else ""))
-    print("IEEE kept (not in the table): CTR :2834, TR :2843, DTV = B/A :2852 -- their numerators "
-          "are products of up to four small factors whose bound falls below 2^-102")
+    print("IEEE kept (not in the table): CTR :2834, TR :2843, DTV = B/A :2852, bare DTG = B/A "
+          ":3198 -- their numerators are sums or products of several possibly small terms "
+          "whose bound falls below 2^-102")
     print(f"derived: FHG >= {fhg_lo:.3g}, CWPC in {cwpc!r}, FV in {fv!r}, RAHC in {rahc!r}, "
           f"RB in {rb!r}")
     if bad:

@@ -32,7 +32,8 @@ def main():
                  5: "ZLVL-ZPD", 6: "HCAN/Z0M/Z0MG/ZPD", 7: "height order", 8: "CWP*VAIE*HCAN",
                  9: "VAIE", 10: "LAISUNE/LAISHAE", 11: "FWET", 12: "FVEG", 13: "SQRT(DLEAF/UC)",
                  14: "RSURF", 16: "RAHG window", 17: "RSSUN/RSSHA", 18: "TV at entry",
-                 19: "TV window"}
+                 19: "TV window", 20: "TGB window (bare)", 21: "bare: air/pressure/wind",
+                 22: "bare: TMPCM..", 23: "bare: heights/RSURF"}
     for kind, n, opt_veg, nsteps in (("mixed", 1 << 20, 1, 25), ("conus", 1 << 20, 1, 25),
                                      ("global", 1_036_800, 2, 25), ("casenml", 65536, 1, 96)):
         eng = Engine(P, dict(L.CASE_NML_OPTIONS, opt_veg=opt_veg), device=0)
@@ -50,7 +51,7 @@ def main():
         torch.cuda.synchronize()
         why = np.zeros(32, np.uint32)
         fb = raw.nmp_debug_fallback_count(1, why.ctypes.data)
-        print(f"{kind:8s} {n:8d} columns x {nsteps} steps: {fb} IEEE re-runs "
+        print(f"{kind:8s} {n:8d} columns x {nsteps} steps: {fb} IEEE loop re-runs (canopy + bare) "
               f"({fb / (n * nsteps):.2e} per column-step), status bits "
               f"{int((cs.status != 0).sum())}", flush=True)
         print("   by condition:", {why_names.get(b, b): int(why[b]) for b in range(32) if why[b]},

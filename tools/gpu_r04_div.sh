@@ -11,5 +11,5 @@ tail -2 "$OUT/pytest_gpu.log"
 NOAHMP_ENGINE_LIB=$PWD/noahmp-1_amd/lib/variants/lib_fbcount.so timeout -k 10 300 \
   python tools/fallback_rate.py > "$OUT/fallback_rate.txt" 2>&1 || { echo "fallback probe failed"; tail "$OUT/fallback_rate.txt"; exit 1; }
 cat "$OUT/fallback_rate.txt"
-TAG=r04_div/ab VARIANTS="vd0 vdnowin" CFGS="3 5" REPS=2 bash tools/variant_ab.sh > "$OUT/ab.txt" 2>&1
+TAG=r04_div/ab VARIANTS="vd0 bare0" CFGS="3 5" REPS=2 bash tools/variant_ab.sh > "$OUT/ab.txt" 2>&1
 cat "$OUT/ab.txt"
