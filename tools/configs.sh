@@ -10,6 +10,8 @@ run() {  # name args...
   local rc=$?; [ $rc -eq 0 ] || { echo "$name rc=$rc"; tail -3 "$OUT/${name}.err"; exit $rc; }
   python -c "import json; d=json.load(open('$OUT/${name}.json')); print('$name', round(d['value']/1e6,1), 'Mcs/s step_ms', round(d['roofline']['step_ms'],3), 'hbm', round(d['roofline']['frac'],4))"
 }
+# config #4 whole: all 4,194,304 CONUS-like columns on one GPU (8 resident forcing slices)
+run cfg4_conus_f32_full_lon-snow-type --kind conus --ncol 4194304 --period 8
 for o in lon-snow-type as-generated; do
   run cfg2_casenml_f64_$o --kind casenml --ncol 65536 --precision 8 --order $o
   run cfg4_conus_f32_$o --kind conus --ncol 524288 --order $o
