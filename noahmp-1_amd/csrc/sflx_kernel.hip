@@ -1532,7 +1532,13 @@ DEV void sflx_column(const DevParams& P, const KArgs<T>& A, Col<T>& c, const Sin
       // outside their window repeats the loop from its start with IEEE
       // division (TV/TAH/EAH reloaded: nothing has stored them yet)
       DivFast32 df;
+#ifdef NMP_VD_NOFALLBACK
+      (void)vege_domain_ok();
+      vege_loop(df);
+      if (false) {  // (timing probe only: not exact in general)
+#else
       if (!(vege_domain_ok() & vege_loop(df))) {
+#endif
 #ifdef NMP_COUNT_FALLBACK
         atomicAdd(&nmp_fallback_ctr, 1u);
         for (int b = 0; b < 20; ++b)
@@ -3028,6 +3034,9 @@ void sflx_step_kernel(const DevParams* __restrict__ gparams,
 #ifdef NMP_WAVE_TIMING
   const unsigned long long wt0 = __builtin_amdgcn_s_memrealtime();
 #endif
+#ifdef NMP_PARAMS_GLOBAL
+  const DevParams& sp = *gparams;
+#else
   __shared__ __attribute__((aligned(16))) DevParams sp;
   {
     const int4* src = reinterpret_cast<const int4*>(gparams);
@@ -3037,6 +3046,7 @@ void sflx_step_kernel(const DevParams* __restrict__ gparams,
   }
   if constexpr (sizeof(T) == 4 && R) stage_math_tables();
   __syncthreads();
+#endif
   int64_t blk = blockIdx.x;
   if (a.order) {
     // re-binned launch: workgroups are dealt round-robin over the 8 XCDs

@@ -81,6 +81,13 @@ struct Mth<float, false> {
 static __shared__ gm::GmTables gm_lds;
 static __constant__ gm::GmTables gm_const = {GM_EXP2F_TAB, GM_LOGF_TAB, GM_POWF_TAB};
 
+// NMP_PARAMS_GLOBAL (probe builds): the tables are read from global memory
+// (L1/L2-resident) instead of being staged per workgroup into LDS
+#ifdef NMP_PARAMS_GLOBAL
+#define NMP_GM_TAB gm_const
+#else
+#define NMP_GM_TAB gm_lds
+#endif
 __device__ __forceinline__ void stage_math_tables() {
   constexpr int NW = sizeof(gm::GmTables) / sizeof(int4);
   static_assert(sizeof(gm::GmTables) % sizeof(int4) == 0, "table size");
@@ -91,14 +98,14 @@ __device__ __forceinline__ void stage_math_tables() {
 
 template <>
 struct Mth<float, true> {
-  NMP_MATH_FN float exp(float x) { return gm::expf(x, gm_lds); }
-  NMP_MATH_FN float exp2(float x) { return gm::exp2f(x, gm_lds); }
-  NMP_MATH_FN float log(float x) { return gm::logf(x, gm_lds); }
-  NMP_MATH_FN float log10(float x) { return gm::log10f(x, gm_lds); }
-  NMP_MATH_FN float pow(float x, float y) { return gm::powf(x, y, gm_lds); }
+  NMP_MATH_FN float exp(float x) { return gm::expf(x, NMP_GM_TAB); }
+  NMP_MATH_FN float exp2(float x) { return gm::exp2f(x, NMP_GM_TAB); }
+  NMP_MATH_FN float log(float x) { return gm::logf(x, NMP_GM_TAB); }
+  NMP_MATH_FN float log10(float x) { return gm::log10f(x, NMP_GM_TAB); }
+  NMP_MATH_FN float pow(float x, float y) { return gm::powf(x, y, NMP_GM_TAB); }
   // bit-exact fp32: the reference's powf itself
-  NMP_MATH_FN float pow_q(float x) { return gm::powf(x, 0.25f, gm_lds); }
-  NMP_MATH_FN float pow_mq(float x) { return gm::powf(x, -0.25f, gm_lds); }
+  NMP_MATH_FN float pow_q(float x) { return gm::powf(x, 0.25f, NMP_GM_TAB); }
+  NMP_MATH_FN float pow_mq(float x) { return gm::powf(x, -0.25f, NMP_GM_TAB); }
   NMP_MATH_FN float tanh(float x) { return gm::tanhf(x); }
   NMP_MATH_FN float atan(float x) { return gm::atanf(x); }
   NMP_MATH_FN float tan(float x) { return gm::tanf(x); }
@@ -236,18 +243,31 @@ struct DivRef {
 // pair of significands, exact scaling by powers of two;
 // profiles/r03/fdiv_exhaust2.txt).
 struct DivFast32 {
-  __device__ __forceinline__ Recip<float> rec(float b) const {
+  __device__ __forceinline__ static float recip(float b) {
     float r = __builtin_amdgcn_rcpf(b);
     const float e = __builtin_fmaf(-b, r, 1.0f);
-    r = __builtin_fmaf(e, r, r);
-    return {b, r};
+    return __builtin_fmaf(e, r, r);
   }
+#ifdef NMP_DIV_NOSHARE
+  // (probe) no shared reciprocal: each quotient forms its own (fewer live
+  // registers, three more instructions per division)
+  __device__ __forceinline__ Recip<float> rec(float b) const { return {b, b}; }
+  __device__ __forceinline__ float div(float a, const Recip<float>& R) const {
+    const float r = recip(R.b);
+    float q = a * r;
+    const float e = __builtin_fmaf(-R.b, q, a);
+    q = __builtin_fmaf(e, r, q);
+    return __builtin_amdgcn_div_fixupf(q, R.b, a);
+  }
+#else
+  __device__ __forceinline__ Recip<float> rec(float b) const { return {b, recip(b)}; }
   __device__ __forceinline__ float div(float a, const Recip<float>& R) const {
     float q = a * R.r;
     const float e = __builtin_fmaf(-R.b, q, a);
     q = __builtin_fmaf(e, R.r, q);
     return __builtin_amdgcn_div_fixupf(q, R.b, a);
   }
+#endif
   __device__ __forceinline__ float divk(float a, const Recip<float>& R) const { return div(a, R); }
   __device__ __forceinline__ void chk(float) const {}
 };

@@ -78,6 +78,12 @@ VARIANTS = {
     # short division became the default)
     "vd0": {"f32": ["-DNMP_VEGE_DIV=0"]},
     "bare0": {"f32": ["-DNMP_BARE_DIV=0"]},
+    # tables read from global memory (no per-workgroup LDS staging), smaller blocks
+    "noshare": {"f32": ["-DNMP_DIV_NOSHARE"]},
+    "vdnofb": {"f32": ["-DNMP_VD_NOFALLBACK"]},
+    "pg": ("-DNMP_PARAMS_GLOBAL",),
+    "pg128": ("-DNMP_PARAMS_GLOBAL", "-DNMP_BLOCK=128"),
+    "pg64": ("-DNMP_PARAMS_GLOBAL", "-DNMP_BLOCK=64"),
     # the default build plus a device counter of lanes that re-ran the canopy
     # loop with IEEE division (nmp_debug_fallback_count)
     "fbcount": {"f32": ["-DNMP_COUNT_FALLBACK"]},

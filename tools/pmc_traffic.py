@@ -7,7 +7,7 @@ write-correction, where the corrections come from the calibration copy
 uncalibrated for non-16B accesses; calibrate on your own pattern).
 FETCH_SIZE/WRITE_SIZE are reported in KB (1024 B) by rocprofv3.
 
-usage: python tools/pmc_traffic.py gpurun_out/<tag> [--ncol N] [--streams S]
+usage: python tools/pmc_traffic.py gpurun_out/<tag> [--ncol N] [--streams S] [--out FILE]
 (S = the bench's --streams: each dispatch covers ncol/S columns)
 """
 import csv
@@ -76,7 +76,14 @@ def main():
     sys.path.insert(0, ROOT)
     import noahmp_pkg  # noqa: F401
     from noahmp_amd import build
-    res = {"source_hash": build.source_hash(), "ncol": ncol, "streams": streams, "kind": kind,
+    # the hash of the library the PMC passes actually measured (the bench line's
+    # checks.build_hash), else the sources here
+    measured = None
+    for lg in glob.glob(os.path.join(base, "bench_*.log")):
+        for ln in open(lg, errors="replace"):
+            if ln.startswith("{") and '"build_hash"' in ln:
+                measured = json.loads(ln)["checks"]["build_hash"]
+    res = {"source_hash": measured or build.source_hash(), "ncol": ncol, "streams": streams, "kind": kind,
            "out_every": out_every, "order": order,
            "precision": 4, "math": "ref", "kernel": KERNEL, "dispatches": nb,
            "fetch_size_kb": bf, "write_size_kb": bw, "read_correction": rf,
@@ -100,6 +107,8 @@ def main():
             except AssertionError:
                 pass
     out = os.path.join(ROOT, "profiles", "traffic.json")
+    if "--out" in sys.argv:
+        out = sys.argv[sys.argv.index("--out") + 1]
     with open(out, "w") as f:
         json.dump(res, f, indent=1)
     print(json.dumps(res, indent=1))
