@@ -1321,6 +1321,10 @@ DEV void sflx_column(const DevParams& P, const KArgs<T>& A, Col<T>& c, const Sin
   c.ch = out.ls(NMP_S_CH); c.tbot = out.lf(NMP_F_TBOT); c.foln = out.lf(NMP_F_FOLN);
   c.co2air = out.la(NMP_A_CO2AIR); c.o2air = out.la(NMP_A_O2AIR);
   NMP_PHASE(4);
+// NMP_DOM_MASK (timing probes only, not exact in general): the checks kept
+#ifndef NMP_DOM_MASK
+#define NMP_DOM_MASK 0xffffffffu
+#endif
 #ifdef NMP_COUNT_FALLBACK
   // (probe builds) which condition sent the lane to an IEEE loop
   unsigned fb_why = 0;
@@ -1331,7 +1335,7 @@ DEV void sflx_column(const DevParams& P, const KArgs<T>& A, Col<T>& c, const Sin
     if (!c_) fb_why |= 1u << (bit);              \
   } while (0)
 #else
-#define NMP_DOM(flag, bit, cond) flag = flag & (cond)
+#define NMP_DOM(flag, bit, cond) flag = flag & (((NMP_DOM_MASK >> (bit)) & 1) == 0 || (cond))
 #endif
   // ---- vege_flux: func.f90:2465-2964 ----
   T tgv = L(0.0), cmv = L(0.0);
@@ -1537,7 +1541,7 @@ DEV void sflx_column(const DevParams& P, const KArgs<T>& A, Col<T>& c, const Sin
       vege_loop(df);
       if (false) {  // (timing probe only: not exact in general)
 #else
-      if (!(vege_domain_ok() & vege_loop(df))) {
+      if (!vege_domain_ok() || !vege_loop(df)) {
 #endif
 #ifdef NMP_COUNT_FALLBACK
         atomicAdd(&nmp_fallback_ctr, 1u);
@@ -1700,7 +1704,7 @@ NMP_UNROLL(NMP_BARE_UNROLL)
 #if NMP_VEGE_DIV && NMP_BARE_DIV
     if constexpr (sizeof(T) == 4 && R && OS != 0) {
       DivFast32 dfb;
-      if (!(bare_domain_ok() & bare_loop(dfb))) {
+      if (!bare_domain_ok() || !bare_loop(dfb)) {
 #ifdef NMP_COUNT_FALLBACK
         atomicAdd(&nmp_fallback_ctr, 1u);
         for (int b = 20; b < 24; ++b)

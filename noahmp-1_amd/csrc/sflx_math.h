@@ -214,11 +214,12 @@ __device__ __forceinline__ double dv<double>(double a, double b) {
 // div_scale / div_fmas / div_fixup sequence, 11 instructions and a vcc chain
 // per division), `dv` in fp64.
 //
-// A faster fp32 policy (a shared v_rcp_f32 reciprocal, one fma residual
-// correction and v_div_fixup, exact while a per-lane range guard holds, with a
-// wave re-run through DivRef when it does not) was built and measured in round
-// 3 and removed: no faster than the IEEE sequence once guarded, and one build
-// of it stepped columns wrong (DESIGN.md "Division in the canopy loop").
+// DivFast32 below is the faster fp32 policy.  Round 3 guarded it dynamically
+// (a per-division range check) and removed it: no faster than IEEE once
+// guarded.  Round 4 proves its operands in range statically (tools/div_proof.py
+// over the domain of vege_domain.h), checks that domain once per column plus a
+// few windows per iteration, and re-runs the loop through DivRef for a lane
+// outside it (DESIGN.md "Division in the Newton loops").
 template <class T>
 struct Recip {
   T b, r;

@@ -81,6 +81,11 @@ VARIANTS = {
     # tables read from global memory (no per-workgroup LDS staging), smaller blocks
     "noshare": {"f32": ["-DNMP_DIV_NOSHARE"]},
     "vdnofb": {"f32": ["-DNMP_VD_NOFALLBACK"]},
+    # domain checks dropped by bit (timing probes only, not exact in general)
+    "dm0_3": {"f32": ["-DNMP_DOM_MASK=0xfffffff0u"]},
+    "dm4_8": {"f32": ["-DNMP_DOM_MASK=0xfffffe0fu"]},
+    "dm9_14": {"f32": ["-DNMP_DOM_MASK=0xffff81ffu"]},
+    "dmwin": {"f32": ["-DNMP_DOM_MASK=0xfff0ffffu"]},
     "pg": ("-DNMP_PARAMS_GLOBAL",),
     "pg128": ("-DNMP_PARAMS_GLOBAL", "-DNMP_BLOCK=128"),
     "pg64": ("-DNMP_PARAMS_GLOBAL", "-DNMP_BLOCK=64"),
