@@ -129,7 +129,8 @@ template <class T>
 __device__ __forceinline__ T p5(T x) { return x * p4(x); }
 
 // Division in the Newton loops (vege_flux, bare_flux, sfcdif1, ragrb).  fp32
-// (the bit-exact path): IEEE `/`.  fp64 (held to tolerances, not bits): the
+// (the bit-exact path): IEEE `/`, except at the range-proven sites that go
+// through DivFast32 (below).  fp64 (held to tolerances, not bits): the
 // reciprocal from v_rcp_f64 refined by two Newton steps, times the numerator,
 // plus one residual correction -- within 1 ulp of the IEEE quotient, in 9
 // instructions instead of the div_scale/div_fmas/div_fixup sequence's 13, and

@@ -128,6 +128,15 @@ VARIANTS = {
     "phifold1_32": {"f32": ["-mllvm", "-two-entry-phi-node-folding-threshold=1"]},
     "specoff32": {"f32": ["-mllvm", "-speculate-one-expensive-inst=false"]},
     "o2": ("-O2",),
+    # round-4 re-sweep on the fp32 translation unit
+    "bu1": {"f32": ["-DNMP_BARE_UNROLL=1"]},
+    "bu3": {"f32": ["-DNMP_BARE_UNROLL=3"]},
+    "vu2_32": {"f32": ["-DNMP_VEGE_UNROLL=2"]},
+    "maxilp32": {"f32": ["-mllvm", "-amdgpu-sched-strategy=max-ilp"]},
+    "exhaust32": {"f32": ["-mllvm", "-exhaustive-register-search"]},
+    "gcprio32": {"f32": ["-mllvm", "-greedy-regclass-priority-trumps-globalness=true"]},
+    "nopostmis32": {"f32": ["-mllvm", "-enable-post-misched=false"]},
+    "w5_32": {"f32": ["-DNMP_WAVES_PER_EU=5"]},
     "gcprio": ("-mllvm", "-greedy-regclass-priority-trumps-globalness=true"),
     # per-wave start/end records (tools/wave_timeline.py)
     "wt": ("-DNMP_WAVE_TIMING",),

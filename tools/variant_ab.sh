@@ -6,12 +6,15 @@ set -u
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 OUT=gpurun_out/${TAG:-vab}; mkdir -p "$OUT"
 CFG5="--kind global --ncol 1036800 --precision 8 --opt-veg 2 --dt 3600 --out-every 1 --forcing device"
+# a variant "lib@VAR=value" runs library lib with that environment variable set
 run() {
-  local name=$1 lib=$2; shift 2
+  local name=$1 spec=$2; shift 2
+  local lib=${spec%%@*} envs=""
+  [ "$spec" != "$lib" ] && envs=${spec#*@}
   if [ "$lib" = default ]; then
-    timeout -k 10 200 python bench.py --no-cpu-baseline "$@" > "$OUT/$name.log" 2>&1
+    env $envs timeout -k 10 200 python bench.py --no-cpu-baseline "$@" > "$OUT/$name.log" 2>&1
   else
-    NOAHMP_ENGINE_LIB=$PWD/noahmp-1_amd/lib/variants/lib_$lib.so timeout -k 10 200 python bench.py --no-cpu-baseline "$@" > "$OUT/$name.log" 2>&1
+    env $envs NOAHMP_ENGINE_LIB=$PWD/noahmp-1_amd/lib/variants/lib_$lib.so timeout -k 10 200 python bench.py --no-cpu-baseline "$@" > "$OUT/$name.log" 2>&1
   fi
   [ $? -eq 0 ] || { echo "$name failed"; tail -3 "$OUT/$name.log"; exit 1; }
   python -c "import json; d=json.loads(open('$OUT/$name.log').read().strip().splitlines()[-1]); print('$name', round(d['value']/1e6,1), 'step_ms', round(d['roofline']['step_ms'],4))"
