@@ -37,6 +37,9 @@ struct SoilRec {  // one soil type (soil_param.f90:13-23)
   // the host with the glibc-exact libm: THKS**(1-SMCMAX) and THKDRY
   float tdf_thks_pow, tdf_thkdry;
   float rsurf_den;  // 2.2E-5*SMCMAX**2*(1-SMCWLT/SMCMAX)**(2+3/BEXP) (rsurf :1150-1151)
+  // THKSAT of an unfrozen layer (SH2O == SMC: XU = SMCMAX, TKICE**0 = 1):
+  // THKS**(1-SMCMAX) * 1 * THKW**SMCMAX, in tdfcnd's own order (func.f90:1564-1569)
+  float tdf_thksat_wet;
   // the same two tdfcnd factors in double for the fp64 path (host libm)
   double tdf_thks_pow_d, tdf_thkdry_d;
 };
@@ -90,6 +93,7 @@ inline void pack_dev_params(const nmp_params& p, DevParams& d) {
     const gm::GmTables& T = kHostGmTables;
     const float thks = gm::powf(7.7f, r.quartz, T) * gm::exp2f(1.0f - r.quartz, T);
     r.tdf_thks_pow = gm::powf(thks, 1.0f - r.smcmax, T);
+    r.tdf_thksat_wet = (r.tdf_thks_pow * gm::powf(2.2f, 0.0f, T)) * gm::powf(0.57f, r.smcmax, T);
     const float gammd = (1.0f - r.smcmax) * 2700.0f;
     r.tdf_thkdry = (0.135f * gammd + 64.7f) / (2700.0f - 0.947f * gammd);
     {

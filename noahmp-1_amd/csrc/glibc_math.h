@@ -231,6 +231,16 @@ GM_HD bool powf_issnan(uint32_t ix) { return 2 * (ix ^ 0x00400000u) > 2u * 0x7fc
 
 GM_HD bool powf_zeroinfnan(uint32_t ix) { return 2 * ix - 1 >= 2u * 0x7f800000u - 1; }
 
+// powf after the log2 of |x|: y*log2(x), the overflow / underflow exits, exp2
+GM_HD float powf_tail(float y, double logx, uint32_t sign_bias, const GmTables& T) {
+  const double ylogx = (double)y * logx;
+  if ((asuint64(ylogx) >> 47 & 0xffff) >= asuint64(126.0) >> 47) {
+    if (ylogx > 0x1.fffffffd1d571p+6) return sign_bias ? -__builtin_inff() : __builtin_inff();
+    if (ylogx <= -150.0) return sign_bias ? -0.0f : 0.0f;
+  }
+  return powf_exp2(ylogx, sign_bias, T);
+}
+
 GM_HD float powf(float x, float y, const GmTables& T) {
   uint32_t sign_bias = 0;
   uint32_t ix = asuint(x), iy = asuint(y);
@@ -260,13 +270,25 @@ GM_HD float powf(float x, float y, const GmTables& T) {
       ix -= 23u << 23;
     }
   }
-  const double logx = powf_log2(ix, T);
-  const double ylogx = (double)y * logx;
-  if ((asuint64(ylogx) >> 47 & 0xffff) >= asuint64(126.0) >> 47) {
-    if (ylogx > 0x1.fffffffd1d571p+6) return sign_bias ? -__builtin_inff() : __builtin_inff();
-    if (ylogx <= -150.0) return sign_bias ? -0.0f : 0.0f;
+  return powf_tail(y, powf_log2(ix, T), sign_bias, T);
+}
+
+// x**y1 and x**y2, each equal to powf's result bit for bit.  When neither
+// call takes powf's special-case block (x positive and normal, y1 and y2
+// nonzero and finite) the log2 of x is formed once: powf's log2 depends on x
+// alone.  (Not glibc code: the sharing is this restatement's, the arithmetic
+// is powf's.)
+GM_HD void powf_pair(float x, float y1, float y2, const GmTables& T, float& r1, float& r2) {
+  const uint32_t ix = asuint(x);
+  if (ix - 0x00800000u < 0x7f800000u - 0x00800000u && !powf_zeroinfnan(asuint(y1)) &&
+      !powf_zeroinfnan(asuint(y2))) {
+    const double logx = powf_log2(ix, T);
+    r1 = powf_tail(y1, logx, 0, T);
+    r2 = powf_tail(y2, logx, 0, T);
+  } else {
+    r1 = powf(x, y1, T);
+    r2 = powf(x, y2, T);
   }
-  return powf_exp2(ylogx, sign_bias, T);
 }
 
 // ---- expm1f / tanhf (fdlibm float; plain fp32 arithmetic, no FMA) ------------

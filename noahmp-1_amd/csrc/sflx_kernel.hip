@@ -247,7 +247,8 @@ DEV Sfc1Inv<T> sfc1_inv(D& d, T sfctmp, T qair, T rhoair, T zlvl, T zpd, T z0h) 
 
 template <class T, bool R, class D>
 DEV void sfcdif1(D& d, const Sfc1Inv<T>& inv, int iter, T h, const Sfc1Logs<T, R>& lg, T ur,
-                 T mpe, T& moz, int& mozsgn, T& fm, T& fh, T& fm2, T& fh2, T& cm, T& ch, T& fv) {
+                 T mpe, T& moz, int& mozsgn, T& fm, T& fh, T& fm2, T& fh2, T& cm, T& ch, T& fv,
+                 bool two_m) {
   typedef Mth<T, R> M;
   T mozold = moz;
   const T tmpcm = lg.tmpcm, tmpch = lg.tmpch, tmpcm2 = lg.tmpcm2, tmpch2 = lg.tmpch2;
@@ -261,7 +262,10 @@ DEV void sfcdif1(D& d, const Sfc1Inv<T>& inv, int iter, T h, const Sfc1Logs<T, R
     if (fabs(tmp1) <= mpe) tmp1 = mpe;
     const Recip<T> rmol = d.rec(d.div(L(-1.0) * p3(fv), d.rec(tmp1)));
     moz = rmin(d.divk(inv.dz, rmol), L(1.0));
-    moz2 = rmin(d.divk(inv.d2, rmol), L(1.0));
+    // the 2-m height's MOZ2 -> FM2/FH2 chain feeds only the 2-m diagnostics
+    // (CHV2/CHB2 -> T2M, Q2): skipped when the step writes no diagnostics
+    // (two_m false, wave-uniform), which changes no state value
+    moz2 = two_m ? rmin(d.divk(inv.d2, rmol), L(1.0)) : L(0.0);
   }
   if (mozold * moz < L(0.0)) mozsgn = mozsgn + 1;
   if (mozsgn >= 2) {
@@ -279,11 +283,15 @@ DEV void sfcdif1(D& d, const Sfc1Inv<T>& inv, int iter, T h, const Sfc1Logs<T, R
     T tmp3 = M::log((L(1.0) + tmp1) / L(2.0));
     fmnew = L(2.0) * tmp3 + tmp2 - L(2.0) * M::atan(tmp1) + L(1.5707963);
     fhnew = L(2.0) * tmp2;
-    T tmp12 = M::pow_q(L(1.0) - L(16.0) * moz2);
-    T tmp22 = M::log((L(1.0) + tmp12 * tmp12) / L(2.0));
-    T tmp32 = M::log((L(1.0) + tmp12) / L(2.0));
-    fm2new = L(2.0) * tmp32 + tmp22 - L(2.0) * M::atan(tmp12) + L(1.5707963);
-    fh2new = L(2.0) * tmp22;
+    if (two_m) {
+      T tmp12 = M::pow_q(L(1.0) - L(16.0) * moz2);
+      T tmp22 = M::log((L(1.0) + tmp12 * tmp12) / L(2.0));
+      T tmp32 = M::log((L(1.0) + tmp12) / L(2.0));
+      fm2new = L(2.0) * tmp32 + tmp22 - L(2.0) * M::atan(tmp12) + L(1.5707963);
+      fh2new = L(2.0) * tmp22;
+    } else {
+      fm2new = fh2new = L(0.0);
+    }
   } else {
     fmnew = L(-5.0) * moz;
     fhnew = fmnew;
@@ -949,6 +957,10 @@ static __device__ unsigned int nmp_fb_reason[32];
 #ifndef NMP_VEGE_UNROLL
 #define NMP_VEGE_UNROLL 1
 #endif
+// NMP_SKIP_2M=0: the 2-m diagnostic chain also on steps without diagnostics (A/B)
+#ifndef NMP_SKIP_2M
+#define NMP_SKIP_2M 1
+#endif
 // Unroll factors of the fixed 5-iteration under-canopy (loop2) and bare_flux
 // Newton loops (tuning knobs, results identical).  bare_flux is unrolled in
 // the fp32 kernels: config #3 +0.8 %, fewer spills (59 -> 52); fp64 and
@@ -1077,6 +1089,9 @@ DEV void sflx_column(const DevParams& P, const KArgs<T>& A, Col<T>& c, const Sin
   const int kt = c.isnow + 3;  // top active layer slot
   T irc = 0, shc = 0, irg = 0, shg = 0, evg = 0, evc = 0, tr = 0, ghv = 0, psnsun = 0, psnsha = 0;
   T t2mv = 0, q2v = 0, chv = 0, chleaf = 0, chuc = 0, chv2 = 0, rssun = 0, rssha = 0;
+  // the 2-m diagnostics (T2M, Q2 and their CHV2/CHB2, FM2/FH2 chain) only
+  // when the step writes diagnostics: nothing else reads them
+  const bool two_m = !NMP_SKIP_2M || out.level != NMP_DIAG_NONE;
   T bgap = 0, wgap = 0;
   T ur = rmax(M::sqrt(c.uu * c.uu + c.vv * c.vv), L(1.0));
   T vai = elai + esai;
@@ -1443,7 +1458,8 @@ DEV void sflx_column(const DevParams& P, const KArgs<T>& A, Col<T>& c, const Sin
       auto vege_iter = [&](const int iter, auto first) -> T {
         if constexpr (!decltype(first)::value) __builtin_assume(iter >= 2);
         if (o.sfc == 1)
-          sfcdif1<T, R>(d, inv, iter, h, lgv, ur, mpe, moz, mozsgn, fm, fh, fm2, fh2, cmv, chv, fv);
+          sfcdif1<T, R>(d, inv, iter, h, lgv, ur, mpe, moz, mozsgn, fm, fh, fm2, fh2, cmv, chv, fv,
+                        two_m);
         if (o.sfc == 2) {
           sfcdif2<T, R>(iter, z0m, c.tah, thair, ur, (T)P.g.czil, zlvl, cmv, chv, moz, wstar, fv);
           chv = chv / ur;
@@ -1590,7 +1606,7 @@ NMP_UNROLL(NMP_LOOP2_UNROLL)
       evg = cev * (estg * rhsur - c.eah);
       ghv = sag - (irg + shg + evg);
     }
-    if (o.sfc == 1 || o.sfc == 2) {
+    if ((o.sfc == 1 || o.sfc == 2) && two_m) {
       chv2 = fv * KARMAN / (((o.sfc == 1) ? lgv.tmpch2 : M::log((L(2.0) + z0h) / z0h)) - fh2);
       if (chv2 < L(1.E-5)) {
         t2mv = c.tah;
@@ -1645,7 +1661,8 @@ NMP_UNROLL(NMP_BARE_UNROLL)
       for (int iter = 1; iter <= 5; ++iter) {
         if constexpr (kFast) NMP_DOM(ok, 20, in(tgb, (T)NMP_DOM_T_LO, (T)NMP_DOM_T_HI));
         if (o.sfc == 1)
-          sfcdif1<T, R>(d, invb, iter, h, lgb, ur, mpe, moz, mozsgn, fm, fh, fm2, fh2, cmb, chb, fv);
+          sfcdif1<T, R>(d, invb, iter, h, lgb, ur, mpe, moz, mozsgn, fm, fh, fm2, fh2, cmb, chb, fv,
+                        two_m);
         if (o.sfc == 2) {
           sfcdif2<T, R>(iter, z0mg, tgb, thair, ur, (T)P.g.czil, zlvl, cmb, chb, moz, wstar, fv);
           chb = chb / ur;
@@ -1725,7 +1742,7 @@ NMP_UNROLL(NMP_BARE_UNROLL)
       evb = cev * (estg * rhsur - eair);
       ghb = sag - (irb + shb + evb);
     }
-    if (o.sfc == 1 || o.sfc == 2) {
+    if ((o.sfc == 1 || o.sfc == 2) && two_m) {
       chb2 = fv * KARMAN / (((o.sfc == 1) ? lgb.tmpch2 : M::log((L(2.0) + z0h) / z0h)) - fh2);
       if (chb2 < L(1.0E-5)) {
         t2mb = tgb;
@@ -2491,9 +2508,14 @@ NMP_UNROLL(NMP_BARE_UNROLL)
     }
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-      T fice = rmin(L(1.0), c.sice[k] / smcmax);
       const T e4 = (sizeof(T) == 4 && R) ? (T)A.c_exp_m4 : M::exp(-L(4.0));
-      fcr[k] = rmax(L(0.0), M::exp(-L(4.0) * (L(1.0) - fice)) - e4) / (L(1.0) - e4);
+      if (NMP_UNFROZEN_FAST && c.sice[k] == L(0.0)) {
+        // no ice: FICE = 0, EXP(-4*(1-FICE)) = EXP(-4) = e4, so FCR = 0 exactly
+        fcr[k] = L(0.0);
+      } else {
+        T fice = rmin(L(1.0), c.sice[k] / smcmax);
+        fcr[k] = rmax(L(0.0), M::exp(-L(4.0) * (L(1.0) - fice)) - e4) / (L(1.0) - e4);
+      }
     }
     T sicemax = L(0.0);
 #pragma unroll
@@ -2596,25 +2618,27 @@ NMP_UNROLL(NMP_BARE_UNROLL)
       T wdf[4], smx[4];
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
+        // FACTR**(BEXP+2) and FACTR**(2 BEXP+3): one base (pow_pair)
+        const T expon1 = bexp + L(2.0), expon2 = L(2.0) * bexp + L(3.0);
         if (o.inf == 1) {  // wdfcnd1
           T factr = rmax(L(0.01), c.smc[k] / smcmax);
-          T expon = bexp + L(2.0);
-          wdf[k] = dwsat * M::pow(factr, expon);
+          T pw1, pw2;
+          pow_pair<T, R>(factr, expon1, expon2, pw1, pw2);
+          wdf[k] = dwsat * pw1;
           wdf[k] = wdf[k] * (L(1.0) - fcr[k]);
-          expon = L(2.0) * bexp + L(3.0);
-          wcnd[k] = dksat * M::pow(factr, expon);
+          wcnd[k] = dksat * pw2;
           wcnd[k] = wcnd[k] * (L(1.0) - fcr[k]);
           smx[k] = c.smc[k];
         } else {  // wdfcnd2
           T factr = rmax(L(0.01), c.sh2o[k] / smcmax);
-          T expon = bexp + L(2.0);
-          wdf[k] = dwsat * M::pow(factr, expon);
+          T pw1, pw2;
+          pow_pair<T, R>(factr, expon1, expon2, pw1, pw2);
+          wdf[k] = dwsat * pw1;
           if (sicemax > L(0.0)) {
             T vkwgt = L(1.0) / (L(1.0) + p3(L(500.0) * sicemax));
-            wdf[k] = vkwgt * wdf[k] + (L(1.0) - vkwgt) * dwsat * M::pow(L(0.2) / smcmax, expon);
+            wdf[k] = vkwgt * wdf[k] + (L(1.0) - vkwgt) * dwsat * M::pow(L(0.2) / smcmax, expon1);
           }
-          expon = L(2.0) * bexp + L(3.0);
-          wcnd[k] = dksat * M::pow(factr, expon);
+          wcnd[k] = dksat * pw2;
           smx[k] = c.sh2o[k];
         }
       }

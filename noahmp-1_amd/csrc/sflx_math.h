@@ -114,6 +114,33 @@ struct Mth<float, true> {
   static __device__ __forceinline__ float sqrt(float x) { return ::sqrtf(x); }
 };
 
+// x**y1 and x**y2 with one base (wdfcnd1/wdfcnd2's WDF and WCND): each equal
+// to Mth::pow's result bit for bit.  The fp32 "ref" path forms powf's log2 of
+// x once (gm::powf_pair); the fp64 path (exp(y log x)) its log once.
+// NMP_POW_PAIR=0: two independent calls (A/B probe).
+#ifndef NMP_POW_PAIR
+#define NMP_POW_PAIR 1
+#endif
+template <class T, bool R>
+__device__ __forceinline__ void pow_pair(T x, T y1, T y2, T& r1, T& r2) {
+#if NMP_POW_PAIR
+  if constexpr (sizeof(T) == 4 && R) {
+    gm::powf_pair(x, y1, y2, NMP_GM_TAB, r1, r2);
+    return;
+  }
+#ifndef NMP_F64_OCML_POW
+  if constexpr (sizeof(T) == 8) {
+    const double lx = ::log(x);
+    r1 = ::exp(y1 * lx);
+    r2 = ::exp(y2 * lx);
+    return;
+  }
+#endif
+#endif
+  r1 = Mth<T, R>::pow(x, y1);
+  r2 = Mth<T, R>::pow(x, y2);
+}
+
 template <class T>
 __device__ __forceinline__ T rmax(T a, T b) { return a > b ? a : b; }
 template <class T>

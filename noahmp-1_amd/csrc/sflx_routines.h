@@ -89,6 +89,11 @@ DEV T esat_val(T t) {
          t * L(1.838826904E-10)))))));
 }
 
+// NMP_UNFROZEN_FAST=0: no unfrozen-layer shortcuts (tdfcnd THKSAT, soilwater FCR):
+// every layer through the powers and exponentials (A/B probe; results identical)
+#ifndef NMP_UNFROZEN_FAST
+#define NMP_UNFROZEN_FAST 1
+#endif
 // tdfcnd: func.f90:1500-1595
 template <class T, bool R>
 DEV T tdfcnd(const SoilRec& S, T smc, T sh2o) {
@@ -101,8 +106,13 @@ DEV T tdfcnd(const SoilRec& S, T smc, T sh2o) {
   T xu = xunfroz * smcmax;
   T thksat, thkdry;
   if constexpr (sizeof(T) == 4 && R) {
-    // soil-type-only factors precomputed on the host (dev_params.h), bit-identical
-    thksat = (T)S.tdf_thks_pow * M::pow(TKICE, smcmax - xu) * M::pow(thkw, xu);
+    // soil-type-only factors precomputed on the host (dev_params.h), bit-identical.
+    // An unfrozen layer (SH2O == SMC, finite and positive) has XUNFROZ = 1 and
+    // XU = SMCMAX exactly, so THKSAT is a soil-type constant too
+    if (NMP_UNFROZEN_FAST && sh2o == smc && smc > L(0.0) && smc <= L(3.0e38))
+      thksat = (T)S.tdf_thksat_wet;
+    else
+      thksat = (T)S.tdf_thks_pow * M::pow(TKICE, smcmax - xu) * M::pow(thkw, xu);
     thkdry = (T)S.tdf_thkdry;
   } else if constexpr (sizeof(T) == 8) {
     // fp64 (tolerance path): the type-only factors from the host in double, and

@@ -128,6 +128,10 @@ VARIANTS = {
     "phifold1_32": {"f32": ["-mllvm", "-two-entry-phi-node-folding-threshold=1"]},
     "specoff32": {"f32": ["-mllvm", "-speculate-one-expensive-inst=false"]},
     "o2": ("-O2",),
+    # probes of the soil-layer math sharing (results identical either way)
+    "nopowpair": ("-DNMP_POW_PAIR=0",),
+    "nounfrozen": ("-DNMP_UNFROZEN_FAST=0",),
+    "no2mskip": ("-DNMP_SKIP_2M=0",),
     # round-4 re-sweep on the fp32 translation unit
     "bu1": {"f32": ["-DNMP_BARE_UNROLL=1"]},
     "bu3": {"f32": ["-DNMP_BARE_UNROLL=3"]},
