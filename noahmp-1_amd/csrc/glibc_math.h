@@ -90,6 +90,12 @@ struct GmTables {
 // ---- expf ------------------------------------------------------------------
 GM_HD uint32_t top12(float x) { return asuint(x) >> 20; }
 
+// GM_BRANCHLESS: the special-case exits of expf/logf as selects after the main
+// path (same results for every input, tests/test_glibc_math.py), so an inlined
+// call is one basic block and consecutive independent calls can interleave
+#ifndef NMP_GM_BRANCHLESS
+#define NMP_GM_BRANCHLESS 0
+#endif
 GM_HD float expf(float x, const GmTables& T) {
   const double InvLn2N = 0x1.71547652b82fep+0 * 32;
   const double SHIFT = 0x1.8p+52;
@@ -97,6 +103,7 @@ GM_HD float expf(float x, const GmTables& T) {
   const double C1 = 0x1.ebfce50fac4f3p-3 / 32 / 32;
   const double C2 = 0x1.62e42ff0c52d6p-1 / 32;
   const double xd = (double)x;
+#if !NMP_GM_BRANCHLESS
   const uint32_t abstop = top12(x) & 0x7ff;
   if (abstop >= top12(88.0f)) {
     if (asuint(x) == asuint(-__builtin_inff())) return 0.0f;
@@ -104,6 +111,7 @@ GM_HD float expf(float x, const GmTables& T) {
     if (x > 0x1.62e42ep6f) return __builtin_inff();  // overflow
     if (x < -0x1.9fe368p6f) return 0.0f;             // underflow
   }
+#endif
   const double z = InvLn2N * xd;
   double kd = z + SHIFT;
   const uint64_t ki = asuint64(kd);
@@ -117,7 +125,16 @@ GM_HD float expf(float x, const GmTables& T) {
   double y = fma_(C2, r, 1.0);
   y = fma_(zz, r2, y);
   y = y * s;
+#if NMP_GM_BRANCHLESS
+  // |x| < 88 never meets the overflow / underflow bounds; -inf underflows to 0
+  // and +inf overflows to inf as x + x would give; NaN -> x + x
+  float res = (float)y;
+  res = x > 0x1.62e42ep6f ? __builtin_inff() : res;
+  res = x < -0x1.9fe368p6f ? 0.0f : res;
+  return x != x ? x + x : res;
+#else
   return (float)y;
+#endif
 }
 
 // ---- exp2f -----------------------------------------------------------------
@@ -153,6 +170,11 @@ GM_HD float logf(float x, const GmTables& T) {
   const double A0 = -0x1.00ea348b88334p-2, A1 = 0x1.5575b0be00b6ap-2, A2 = -0x1.ffffef20a4123p-2;
   const uint32_t OFF = 0x3f330000;
   uint32_t ix = asuint(x);
+#if NMP_GM_BRANCHLESS
+  const uint32_t ix0 = ix;
+  const bool outside = ix - 0x00800000u >= 0x7f800000u - 0x00800000u;
+  ix = outside ? asuint(x * 0x1p23f) - (23u << 23) : ix;  // subnormal: normalize
+#else
   if (ix == 0x3f800000) return 0.0f;
   if (ix - 0x00800000u >= 0x7f800000u - 0x00800000u) {
     if (ix * 2 == 0) return -__builtin_inff();
@@ -161,6 +183,7 @@ GM_HD float logf(float x, const GmTables& T) {
     ix = asuint(x * 0x1p23f);  // subnormal: normalize
     ix -= 23u << 23;
   }
+#endif
   const uint32_t tmp = ix - OFF;
   const int i = (tmp >> (23 - 4)) % 16;
   const int k = (int32_t)tmp >> 23;
@@ -173,7 +196,17 @@ GM_HD float logf(float x, const GmTables& T) {
   double y = fma_(A1, r, A2);
   y = fma_(A0, r2, y);
   y = fma_(y, r2, y0 + r);
+#if NMP_GM_BRANCHLESS
+  // x = 1 gives +0 through the main path as the early return does; the
+  // outside-range inputs: +-0 -> -inf, +inf -> x, negative or NaN -> NaN,
+  // positive subnormal -> the normalized main path
+  const float res = (float)y;
+  const float nan_or = ((ix0 & 0x80000000u) || ix0 * 2 >= 0xff000000u) ? __builtin_nanf("") : res;
+  const float sp = ix0 * 2 == 0 ? -__builtin_inff() : ix0 == 0x7f800000 ? x : nan_or;
+  return outside ? sp : res;
+#else
   return (float)y;
+#endif
 }
 
 // ---- powf ------------------------------------------------------------------

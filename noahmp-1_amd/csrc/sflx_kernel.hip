@@ -1089,9 +1089,9 @@ DEV void sflx_column(const DevParams& P, const KArgs<T>& A, Col<T>& c, const Sin
   const int kt = c.isnow + 3;  // top active layer slot
   T irc = 0, shc = 0, irg = 0, shg = 0, evg = 0, evc = 0, tr = 0, ghv = 0, psnsun = 0, psnsha = 0;
   T t2mv = 0, q2v = 0, chv = 0, chleaf = 0, chuc = 0, chv2 = 0, rssun = 0, rssha = 0;
-  // the 2-m diagnostics (T2M, Q2 and their CHV2/CHB2, FM2/FH2 chain) only
-  // when the step writes diagnostics: nothing else reads them
-  const bool two_m = !NMP_SKIP_2M || out.level != NMP_DIAG_NONE;
+  // the diagnostic-only chains (the 2-m MOZ2 -> FH2 -> CHV2/CHB2 -> T2M, Q2;
+  // TRAD) only when the step writes diagnostics: nothing else reads them
+  const bool diag_on = !NMP_SKIP_2M || out.level != NMP_DIAG_NONE;
   T bgap = 0, wgap = 0;
   T ur = rmax(M::sqrt(c.uu * c.uu + c.vv * c.vv), L(1.0));
   T vai = elai + esai;
@@ -1459,7 +1459,7 @@ DEV void sflx_column(const DevParams& P, const KArgs<T>& A, Col<T>& c, const Sin
         if constexpr (!decltype(first)::value) __builtin_assume(iter >= 2);
         if (o.sfc == 1)
           sfcdif1<T, R>(d, inv, iter, h, lgv, ur, mpe, moz, mozsgn, fm, fh, fm2, fh2, cmv, chv, fv,
-                        two_m);
+                        diag_on);
         if (o.sfc == 2) {
           sfcdif2<T, R>(iter, z0m, c.tah, thair, ur, (T)P.g.czil, zlvl, cmv, chv, moz, wstar, fv);
           chv = chv / ur;
@@ -1606,7 +1606,7 @@ NMP_UNROLL(NMP_LOOP2_UNROLL)
       evg = cev * (estg * rhsur - c.eah);
       ghv = sag - (irg + shg + evg);
     }
-    if ((o.sfc == 1 || o.sfc == 2) && two_m) {
+    if ((o.sfc == 1 || o.sfc == 2) && diag_on) {
       chv2 = fv * KARMAN / (((o.sfc == 1) ? lgv.tmpch2 : M::log((L(2.0) + z0h) / z0h)) - fh2);
       if (chv2 < L(1.E-5)) {
         t2mv = c.tah;
@@ -1662,7 +1662,7 @@ NMP_UNROLL(NMP_BARE_UNROLL)
         if constexpr (kFast) NMP_DOM(ok, 20, in(tgb, (T)NMP_DOM_T_LO, (T)NMP_DOM_T_HI));
         if (o.sfc == 1)
           sfcdif1<T, R>(d, invb, iter, h, lgb, ur, mpe, moz, mozsgn, fm, fh, fm2, fh2, cmb, chb, fv,
-                        two_m);
+                        diag_on);
         if (o.sfc == 2) {
           sfcdif2<T, R>(iter, z0mg, tgb, thair, ur, (T)P.g.czil, zlvl, cmb, chb, moz, wstar, fv);
           chb = chb / ur;
@@ -1742,7 +1742,7 @@ NMP_UNROLL(NMP_BARE_UNROLL)
       evb = cev * (estg * rhsur - eair);
       ghb = sag - (irb + shb + evb);
     }
-    if ((o.sfc == 1 || o.sfc == 2) && two_m) {
+    if ((o.sfc == 1 || o.sfc == 2) && diag_on) {
       chb2 = fv * KARMAN / (((o.sfc == 1) ? lgb.tmpch2 : M::log((L(2.0) + z0h) / z0h)) - fh2);
       if (chb2 < L(1.0E-5)) {
         t2mb = tgb;
@@ -1790,7 +1790,7 @@ NMP_UNROLL(NMP_BARE_UNROLL)
   if (fire <= L(0.0)) c.status |= NMP_ST_FIRE;
   T emissi = fveg * (emg * (L(1.) - emv) + emv + emv * (L(1.) - emv) * (L(1.) - emg)) +
              (L(1.) - fveg) * emg;
-  T trad = M::pow_q((fire - (L(1.0) - emissi) * c.lwdn) / (emissi * SB));
+  T trad = diag_on ? M::pow_q((fire - (L(1.0) - emissi) * c.lwdn) / (emissi * SB)) : L(0.0);
   T apar = parsun * laisun + parsha * laisha;
   T psn = psnsun * laisun + psnsha * laisha;
   // error(): energy balance (func.f90:712-721), a function of final energy terms only

@@ -85,9 +85,46 @@ static int check_powf(unsigned stride) {
   return bad ? 1 : 0;
 }
 
+// powf_pair: every x on a stride, for pairs of exponents (wdfcnd's BEXP+2 and
+// 2*BEXP+3 over the table's BEXP values, and special exponents), both results
+// against host powf
+static int check_powf_pair(unsigned stride) {
+  const float bexps[] = {2.79f, 4.26f, 4.74f, 5.33f, 5.25f, 6.77f, 8.72f, 8.17f, 10.73f, 10.39f,
+                         11.55f, 12.61f, 2.79f, 4.26f, 11.55f, 2.5f};
+  const float extra[][2] = {{0.0f, 1.0f}, {1.0f, 0.0f}, {-2.0f, 3.0f}, {0.25f, -0.25f},
+                            {INFINITY, 2.0f}, {2.0f, NAN}, {1e-3f, 33.0f}};
+  unsigned long long bad = 0, n = 0;
+  const int nb = sizeof(bexps) / sizeof(bexps[0]), ne = sizeof(extra) / sizeof(extra[0]);
+  for (int j = 0; j < nb + ne; ++j) {
+    const float y1 = j < nb ? bexps[j] + 2.0f : extra[j - nb][0];
+    const float y2 = j < nb ? 2.0f * bexps[j] + 3.0f : extra[j - nb][1];
+#pragma omp parallel for reduction(+ : bad, n) schedule(static, 65536)
+    for (long long i = 0; i < (1LL << 32); i += stride) {
+      const unsigned u = (unsigned)i;
+      float x;
+      memcpy(&x, &u, 4);
+      float a1, a2;
+      gm::powf_pair(x, y1, y2, T, a1, a2);
+      const float b1 = ::powf(x, y1), b2 = ::powf(x, y2);
+      unsigned ua1, ub1, ua2, ub2;
+      memcpy(&ua1, &a1, 4);
+      memcpy(&ub1, &b1, 4);
+      memcpy(&ua2, &a2, 4);
+      memcpy(&ub2, &b2, 4);
+      n += 2;
+      if (!(ua1 == ub1 || (isnan(a1) && isnan(b1)))) bad++;
+      if (!(ua2 == ub2 || (isnan(a2) && isnan(b2)))) bad++;
+    }
+  }
+  printf("powf_pair mismatches %llu of %llu\n", bad, n);
+  return bad ? 1 : 0;
+}
+
 int main(int argc, char** argv) {
   if (argc < 2) return 2;
   if (!strcmp(argv[1], "powf")) return check_powf(argc > 2 ? (unsigned)atoi(argv[2]) : 3);
+  if (!strcmp(argv[1], "powf_pair"))
+    return check_powf_pair(argc > 2 ? (unsigned)atoi(argv[2]) : 3);
   const unsigned stride = argc > 2 ? (unsigned)atoi(argv[2]) : 1;
   for (const Entry& e : FUNCS) {
     if (strcmp(e.name, argv[1])) continue;

@@ -132,6 +132,7 @@ VARIANTS = {
     "nopowpair": ("-DNMP_POW_PAIR=0",),
     "nounfrozen": ("-DNMP_UNFROZEN_FAST=0",),
     "no2mskip": ("-DNMP_SKIP_2M=0",),
+    "gmbl": ("-DNMP_GM_BRANCHLESS=1",),
     # round-4 re-sweep on the fp32 translation unit
     "bu1": {"f32": ["-DNMP_BARE_UNROLL=1"]},
     "bu3": {"f32": ["-DNMP_BARE_UNROLL=3"]},
