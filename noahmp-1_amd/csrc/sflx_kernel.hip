@@ -1002,7 +1002,11 @@ DEV void sflx_column(const DevParams& P, const KArgs<T>& A, Col<T>& c, const Sin
 
   // atm: func.f90:479-531
   T pair = c.sfcprs;
-  T thair = c.sfctmp * M::pow(c.sfcprs / pair, RAIR / CPAIR);
+  // PAIR = SFCPRS: the ratio is exactly 1 for a finite nonzero pressure and
+  // powf(1, y) = 1, so THAIR = SFCTMP * 1 = SFCTMP (other pressures: as written)
+  T thair = (c.sfcprs != L(0.0) && fabs(c.sfcprs) <= L(3.0e38))
+                ? c.sfctmp
+                : c.sfctmp * M::pow(c.sfcprs / pair, RAIR / CPAIR);
   T qair = c.q2;
   T eair = qair * c.sfcprs / (L(0.622) + L(0.378) * qair);
   T rhoair = (c.sfcprs - L(0.378) * eair) / (RAIR * c.sfctmp);
@@ -1057,7 +1061,8 @@ DEV void sflx_column(const DevParams& P, const KArgs<T>& A, Col<T>& c, const Sin
     T db = rmin(rmax(c.snowh - hvb, L(0.0)), hvt - hvb);
     T fb = db / rmax(L(1.0E-06), hvt - hvb);
     if (hvt > L(0.0) && hvt <= L(1.0)) {
-      T snowhc = hvt * M::exp(-c.snowh / L(0.2));
+      // no snow: EXP(-0) = 1 exactly (the exponential skipped)
+      T snowhc = hvt * (c.snowh == L(0.0) ? L(1.0) : M::exp(-c.snowh / L(0.2)));
       fb = rmin(c.snowh, snowhc) / snowhc;
     }
     elai = c.lai * (L(1.0) - fb);
@@ -1267,7 +1272,8 @@ DEV void sflx_column(const DevParams& P, const KArgs<T>& A, Col<T>& c, const Sin
   out.template d<NMP_D_FVEG>(fveg);
   out.template d<NMP_D_BGAP>(bgap);
   out.template d<NMP_D_WGAP>(wgap);
-  T emv = L(1.0) - M::exp(-(elai + esai) / L(1.0));
+  // no leaves or stems: EXP(-0) = 1 and EMV = +0 exactly (the exponential skipped)
+  T emv = (elai + esai == L(0.0)) ? L(0.0) : L(1.0) - M::exp(-(elai + esai) / L(1.0));
   T emg;
   if (c.ice == 1)
     emg = L(0.98) * (L(1.0) - fsno) + L(1.0) * fsno;
@@ -2176,7 +2182,10 @@ NMP_UNROLL(NMP_BARE_UNROLL)
     T maxliq = (T)V.canwmxp * (elai + esai);
     if ((elai + esai) > L(0.0)) {
       qintr = fveg * rain * fp;
-      qintr = rmin(qintr, (maxliq - c.canliq) / DT * (L(1.0) - M::exp(-rain * DT / maxliq)));
+      // no rain: EXP(-0) = 1 makes the bound +-0 (or NaN), and QINTR ends +0
+      // through the MAX below either way, so the exponential is skipped
+      if (rain != L(0.0))
+        qintr = rmin(qintr, (maxliq - c.canliq) / DT * (L(1.0) - M::exp(-rain * DT / maxliq)));
       qintr = rmax(qintr, L(0.0));
       qdripr = fveg * rain - qintr;
       qthror = (L(1.0) - fveg) * rain;
@@ -2204,7 +2213,8 @@ NMP_UNROLL(NMP_BARE_UNROLL)
     T maxsno = L(6.6) * (L(0.27) + L(46.0) / bdfall) * (elai + esai);
     if ((elai + esai) > L(0.0)) {
       qints = fveg * snow * fp;
-      qints = rmin(qints, (maxsno - c.canice) / DT * (L(1.0) - M::exp(-snow * DT / maxsno)));
+      if (snow != L(0.0))  // as QINTR: no snow leaves QINTS = +0
+        qints = rmin(qints, (maxsno - c.canice) / DT * (L(1.0) - M::exp(-snow * DT / maxsno)));
       qints = rmax(qints, L(0.0));
       T ft = rmax(L(0.0), (c.tv - L(270.15)) / L(1.87E5));
       T fvw = M::sqrt(uu_w * uu_w + vv_w * vv_w) / L(1.56E5);
