@@ -464,9 +464,9 @@ DEV StomataPre<T> stomata_pre(const VegRec& V, bool any_light, T sfcprs, T sfctm
   return p;
 }
 
-template <class T, bool R>
-DEV void stomata_solve(const VegRec& V, const StomataPre<T>& p, T igs, T sfcprs, T apar, T ea,
-                       T ei, T co2, T& rs, T& psn) {
+template <class T, bool R, class D>
+DEV void stomata_solve(D& d, const VegRec& V, const StomataPre<T>& p, T igs, T sfcprs, T apar,
+                       T ea, T ei, T co2, T& rs, T& psn) {
   typedef Mth<T, R> M;
   const T CIERR = L(5.0E-2);
   const T cf = p.cf;
@@ -485,23 +485,23 @@ DEV void stomata_solve(const VegRec& V, const StomataPre<T>& p, T igs, T sfcprs,
     T ci = L(0.5) * (cihigh + cilow);
     T wc = (T)NAN, wj = (T)NAN, we = (T)NAN;  // SAVEd nan4 init (func.f90:3854-3856)
     if (c3c4 == 1) {
-      wj = rmax(ci - cp, L(0.0)) * j / (ci + L(2.0) * cp);
-      wc = rmax(ci - cp, L(0.0)) * vcmx / (ci + awc);
+      wj = d.div(rmax(ci - cp, L(0.0)) * j, d.rec(ci + L(2.0) * cp));
+      wc = d.div(rmax(ci - cp, L(0.0)) * vcmx, d.rec(ci + awc));
       we = L(0.5) * vcmx;
     } else if (c3c4 == 2) {
       wj = j;
       wc = vcmx;
-      we = L(4000.0) * vcmx * ci / sfcprs;
+      we = d.div(L(4000.0) * vcmx * ci, d.rec(sfcprs));
     }
     psn = rmin(rmin(wj, wc), we) * igs;
     T cs = rmax(co2 - L(1.37) * rlb * sfcprs * psn, MPE);
-    T a = mp * psn * sfcprs * ea / (cs * ei) + bp;
-    T b = (mp * psn * sfcprs / cs + bp) * rlb - L(1.0);
+    T a = d.div(mp * psn * sfcprs * ea, d.rec(cs * ei)) + bp;
+    T b = (d.div(mp * psn * sfcprs, d.rec(cs)) + bp) * rlb - L(1.0);
     T c = -rlb;
     T q = (b >= L(0.0)) ? L(-0.5) * (b + M::sqrt(b * b - L(4.0) * a * c))
                         : L(-0.5) * (b - M::sqrt(b * b - L(4.0) * a * c));
-    T r1 = q / a;
-    T r2 = c / q;
+    T r1 = d.div(q, d.rec(a));
+    T r2 = d.div(c, d.rec(q));
     rs = rmax(r1, r2);
     T fci = rmax(cs - psn * sfcprs * L(1.65) * rs, L(0.0));
     if (((cihigh - cilow) <= CIERR) || fabs(fci - ci) <= MPE) break;
@@ -1486,8 +1486,16 @@ DEV void sflx_column(const DevParams& P, const KArgs<T>& A, Col<T>& c, const Sin
             const StomataPre<T> sp =
                 stomata_pre<T, R>(V, parsun > L(0.0) || parsha > L(0.0), c.sfcprs, c.sfctmp, c.tv,
                                   c.o2air, c.foln, btran, rb);
-            stomata_solve<T, R>(V, sp, igs, c.sfcprs, parsun, c.eah, estv, c.co2air, rssun, psnsun);
-            stomata_solve<T, R>(V, sp, igs, c.sfcprs, parsha, c.eah, estv, c.co2air, rssha, psnsha);
+#ifdef NMP_STOMATA_FASTDIV
+            // (timing probe only: the bisection's divisions unguarded, not exact in general)
+            std::conditional_t<sizeof(T) == 4 && R, DivFast32, DivRef<T>> dst;
+#else
+            DivRef<T> dst;
+#endif
+            stomata_solve<T, R>(dst, V, sp, igs, c.sfcprs, parsun, c.eah, estv, c.co2air, rssun,
+                                psnsun);
+            stomata_solve<T, R>(dst, V, sp, igs, c.sfcprs, parsha, c.eah, estv, c.co2air, rssha,
+                                psnsha);
           }
           if (o.crs == 2) {
             canres<T, R>(V, c.sfcprs, c.tv, parsun, c.eah, btran, rssun, psnsun);

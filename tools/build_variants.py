@@ -133,6 +133,7 @@ VARIANTS = {
     "nounfrozen": ("-DNMP_UNFROZEN_FAST=0",),
     "no2mskip": ("-DNMP_SKIP_2M=0",),
     "gmbl": ("-DNMP_GM_BRANCHLESS=1",),
+    "stfast": {"f32": ["-DNMP_STOMATA_FASTDIV"]},
     # round-4 re-sweep on the fp32 translation unit
     "bu1": {"f32": ["-DNMP_BARE_UNROLL=1"]},
     "bu3": {"f32": ["-DNMP_BARE_UNROLL=3"]},
