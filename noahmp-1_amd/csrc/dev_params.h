@@ -7,6 +7,7 @@
 // ~9 KB and is staged into LDS once per workgroup; every lane then gathers its
 // own type's fields from LDS with ds_read (per-lane addresses, no HBM traffic).
 #pragma once
+#include "vege_domain.h"
 #include <stdint.h>
 
 #include <cmath>
@@ -25,6 +26,9 @@ struct VegRec {  // one USGS/MODIS vegetation type (veg_param.f90:19-74)
   float kc25, akc, ko25, ako, vcmx25, avcmx, bp, mp, qe25, folnmx, tmin;
   float rmf25, rms25, rmr25, arm, mrp;
   int32_t nroot, c3c4;
+  // 1: the parameters lie in the stomata bisection's proven box
+  // (vege_domain.h, tools/div_proof.py), so its divisions may be short
+  int32_t stomata_fast, pad_;
   // veg-type-only transcendentals, evaluated once on the host (glibc-exact):
   // twostream AVMU (:2338-2341), LOG(HVT/Z0MVT) (vege_flux UC :2725) and
   // LOG((2+Z0M)/Z0M) (sfcdif1 TMPCM2 :3419 with Z0M = Z0MVT)
@@ -129,6 +133,18 @@ inline void pack_dev_params(const nmp_params& p, DevParams& d) {
     r.rmf25 = p.rmf25[v]; r.rms25 = p.rms25[v]; r.rmr25 = p.rmr25[v]; r.arm = p.arm[v];
     r.mrp = p.mrp[v];
     r.nroot = p.nroot[v]; r.c3c4 = p.c3c4[v];
+    {
+      auto in = [](float x, double lo, double hi) { return x >= (float)lo && x <= (float)hi; };
+      r.stomata_fast =
+          in(r.kc25, NMP_DOM_KC25_LO, NMP_DOM_KC25_HI) && in(r.akc, NMP_DOM_AKC_LO, NMP_DOM_AKC_HI) &&
+          in(r.ko25, NMP_DOM_KO25_LO, NMP_DOM_KO25_HI) && in(r.ako, NMP_DOM_AKO_LO, NMP_DOM_AKO_HI) &&
+          in(r.avcmx, NMP_DOM_AVCMX_LO, NMP_DOM_AVCMX_HI) && in(r.mp, NMP_DOM_MP_LO, NMP_DOM_MP_HI) &&
+          in(r.bp, NMP_DOM_BP_LO, NMP_DOM_BP_HI) &&
+          (r.qe25 == 0.0f || in(r.qe25, NMP_DOM_QE25_LO, NMP_DOM_QE25_HI)) &&
+          (r.vcmx25 == 0.0f || (in(r.vcmx25, NMP_DOM_VCMX25_LO, NMP_DOM_VCMX25_HI) &&
+                                in(r.tmin, NMP_DOM_TMIN_LO, NMP_DOM_TMIN_HI)));
+      r.pad_ = 0;
+    }
     {
       const gm::GmTables& T = kHostGmTables;
       float chil = r.xl > -0.4f ? r.xl : -0.4f;  // rmin(rmax(XL,-0.4),0.6) as the kernel

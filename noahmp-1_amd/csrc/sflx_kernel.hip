@@ -439,6 +439,7 @@ DEV void ragrb(D& d, const Recip<T>& rhocp, const Recip<T>& rhcan, T dzg, T sqrt
 template <class T>
 struct StomataPre {
   T cf, kc, ko, awc, cp, vcmx, rlb;
+  T fnf;  // MIN(FOLN / MAX(MPE, FOLNMX), 1) (the short-division domain check)
 };
 
 template <class T, bool R>
@@ -447,9 +448,10 @@ DEV StomataPre<T> stomata_pre(const VegRec& V, bool any_light, T sfcprs, T sfctm
   typedef Mth<T, R> M;
   StomataPre<T> p;
   p.cf = sfcprs / (RGAS * sfctmp) * L(1.0e06);
-  p.kc = p.ko = p.awc = p.cp = p.vcmx = p.rlb = L(0.0);
+  p.kc = p.ko = p.awc = p.cp = p.vcmx = p.rlb = p.fnf = L(0.0);
   if (any_light) {
     T fnf = rmin(foln / rmax(MPE, (T)V.folnmx), L(1.0));
+    p.fnf = fnf;
     T tc = tv - TFRZ;
     T ex = (tc - L(25.0)) / L(10.0);
     p.kc = (T)V.kc25 * M::pow((T)V.akc, ex);
@@ -1486,16 +1488,42 @@ DEV void sflx_column(const DevParams& P, const KArgs<T>& A, Col<T>& c, const Sin
             const StomataPre<T> sp =
                 stomata_pre<T, R>(V, parsun > L(0.0) || parsha > L(0.0), c.sfcprs, c.sfctmp, c.tv,
                                   c.o2air, c.foln, btran, rb);
+            // The bisection's divisions: short (DivFast32) in the fast canopy loop
+            // when the column and its vegetation type lie in the proven domain
+            // (vege_domain.h "stomata", tools/div_proof.py), IEEE otherwise.
+            DivRef<T> dsr;
+            bool st_fast = false;
+            if constexpr (std::is_same_v<std::decay_t<decltype(d)>, DivFast32>) {
+              auto in = [](T x, double lo, double hi) { return x >= (T)lo && x <= (T)hi; };
+              auto apar_ok = [&](T x) {
+                return x <= L(0.0) || in(x, NMP_DOM_APAR_LO, NMP_DOM_APAR_HI);
+              };
+              st_fast = V.stomata_fast && c.tv <= (T)NMP_DOM_STOMATA_TV_HI &&
+                        (c.eah == L(0.0) || in(c.eah, NMP_DOM_EAH_LO, NMP_DOM_EAH_HI)) &&
+                        in(c.co2air, NMP_DOM_CO2_LO, NMP_DOM_CO2_HI) &&
+                        in(c.o2air, NMP_DOM_O2_LO, NMP_DOM_O2_HI) &&
+                        (sp.fnf == L(0.0) || in(sp.fnf, NMP_DOM_FNF_LO, 1.0)) &&
+                        apar_ok(parsun) && apar_ok(parsha);
 #ifdef NMP_STOMATA_FASTDIV
-            // (timing probe only: the bisection's divisions unguarded, not exact in general)
-            std::conditional_t<sizeof(T) == 4 && R, DivFast32, DivRef<T>> dst;
-#else
-            DivRef<T> dst;
+              st_fast = true;  // (timing probe only: not exact in general)
 #endif
-            stomata_solve<T, R>(dst, V, sp, igs, c.sfcprs, parsun, c.eah, estv, c.co2air, rssun,
-                                psnsun);
-            stomata_solve<T, R>(dst, V, sp, igs, c.sfcprs, parsha, c.eah, estv, c.co2air, rssha,
-                                psnsha);
+#ifdef NMP_COUNT_FALLBACK
+              if (!st_fast && (parsun > L(0.0) || parsha > L(0.0)))
+                atomicAdd(&nmp_fb_reason[24], 1u);  // stomata bisection on IEEE division
+#endif
+              if (st_fast) {
+                stomata_solve<T, R>(d, V, sp, igs, c.sfcprs, parsun, c.eah, estv, c.co2air,
+                                    rssun, psnsun);
+                stomata_solve<T, R>(d, V, sp, igs, c.sfcprs, parsha, c.eah, estv, c.co2air,
+                                    rssha, psnsha);
+              }
+            }
+            if (!st_fast) {
+              stomata_solve<T, R>(dsr, V, sp, igs, c.sfcprs, parsun, c.eah, estv, c.co2air,
+                                  rssun, psnsun);
+              stomata_solve<T, R>(dsr, V, sp, igs, c.sfcprs, parsha, c.eah, estv, c.co2air,
+                                  rssha, psnsha);
+            }
           }
           if (o.crs == 2) {
             canres<T, R>(V, c.sfcprs, c.tv, parsun, c.eah, btran, rssun, psnsun);

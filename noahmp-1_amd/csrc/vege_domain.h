@@ -1,5 +1,5 @@
 // The input domain of the canopy Newton loop's short divisions (sflx_kernel.hip
-// vege_flux, DivFast32 in sflx_math.h).
+// vege_flux, DivFast32 in sflx_math.h), and below it the stomata bisection's.
 //
 // Every division of the loop (vege_flux with its sfcdif1 and ragrb,
 // func.f90:2744-2877, :3353-3508, :3260-3350) is exact in the short sequence
@@ -56,3 +56,50 @@
 // ground aerodynamic resistance RAHG (s m-1), every iteration
 #define NMP_DOM_RAHG_LO 1.0e-3
 #define NMP_DOM_RAHG_HI 1.0e10
+
+// ---- the stomata bisection (stomata, func.f90:3739-3887; sflx_kernel.hip
+// stomata_solve), run in the canopy loop's first iteration.  Its six divisions
+// per bisection step use DivFast32 when, besides the canopy loop's domain
+// above, the column's inputs lie in the limits below (checked once, before the
+// two calls; a lane outside them runs the bisection with IEEE division) and
+// its vegetation type's parameters lie in the box below (checked on the host,
+// VegRec::stomata_fast).  tools/div_proof.py proves the sites per 1 K band of
+// the canopy temperature.
+// absorbed PAR per leaf area, PARSUN / PARSHA (W m-2): <= 0 (no bisection) or in
+#define NMP_DOM_APAR_LO 1.0e-6
+#define NMP_DOM_APAR_HI 1.0e4
+// canopy-air vapour pressure EAH (Pa) at the first iteration: 0 or in
+#define NMP_DOM_EAH_LO 1.0e-2
+#define NMP_DOM_EAH_HI 1.5e4
+// CO2 and O2 partial pressures (Pa)
+#define NMP_DOM_CO2_LO 1.0
+#define NMP_DOM_CO2_HI 1.0e3
+#define NMP_DOM_O2_LO 1.0e3
+#define NMP_DOM_O2_HI 1.0e5
+// foliage nitrogen factor FNF = MIN(FOLN / MAX(MPE, FOLNMX), 1): 0 or >= this
+#define NMP_DOM_FNF_LO 1.0e-3
+// canopy temperature TV at the first iteration (K): <= this (VCMX's
+// high-temperature factor 1 + EXP(...) reaches 2e3 at 340 K, 1e14 at 500 K)
+#define NMP_DOM_STOMATA_TV_HI 340.0
+// vegetation-type parameters (VEGPARM.TBL; every shipped table lies inside)
+#define NMP_DOM_KC25_LO 20.0
+#define NMP_DOM_KC25_HI 40.0
+#define NMP_DOM_AKC_LO 2.0
+#define NMP_DOM_AKC_HI 2.2
+#define NMP_DOM_KO25_LO 2.0e4
+#define NMP_DOM_KO25_HI 4.0e4
+#define NMP_DOM_AKO_LO 1.1
+#define NMP_DOM_AKO_HI 1.3
+#define NMP_DOM_AVCMX_LO 2.3
+#define NMP_DOM_AVCMX_HI 2.5
+#define NMP_DOM_VCMX25_LO 1.0
+#define NMP_DOM_VCMX25_HI 200.0
+#define NMP_DOM_QE25_LO 1.0e-3
+#define NMP_DOM_QE25_HI 0.2
+#define NMP_DOM_MP_LO 1.0
+#define NMP_DOM_MP_HI 20.0
+#define NMP_DOM_BP_LO 100.0
+#define NMP_DOM_BP_HI 1.0e16
+// TMIN (K) of a type with VCMX25 > 0: PSN > 0 needs IGS = 1, i.e. TV > TMIN
+#define NMP_DOM_TMIN_LO 250.0
+#define NMP_DOM_TMIN_HI 300.0

@@ -998,7 +998,7 @@ def test_tiny_canopy_wet_fraction_bit_exact(engines, oracle_port, fwet, variant)
 
 
 @pytest.mark.parametrize("variant", VARIANTS)
-@pytest.mark.parametrize("perturb", ["wind", "pressure", "fwet", "mixed"])
+@pytest.mark.parametrize("perturb", ["wind", "pressure", "fwet", "co2", "eah", "mixed"])
 def test_canopy_division_domain_fallback_bit_exact(engines, oracle_port, perturb, variant):
     """The canopy Newton loop divides with the short exact sequence inside the
     range proof's domain (csrc/vege_domain.h, tools/div_proof.py) and falls
@@ -1006,7 +1006,9 @@ def test_canopy_division_domain_fallback_bit_exact(engines, oracle_port, perturb
     domain -- wind of 150-400 m/s, surface pressure of 2.5e4 Pa, a canopy wet
     fraction of 1e-20, or all three on different columns -- next to untouched
     ones: every column equals the C restatement bit for bit, in both
-    occupancy instantiations."""
+    occupancy instantiations.  CO2 = 0.5 Pa and EAH = 1e-5 Pa stay inside the
+    canopy loop's domain but leave the stomata bisection's, which then
+    divides with IEEE division alone."""
     P = __import__("noahmp_amd.params", fromlist=["Params"]).Params.builtin()
     from noahmp_amd.engine import ColumnState
     opts = [L.CASE_NML_OPTIONS[k] for k in L.OPTION_NAMES]
@@ -1017,13 +1019,17 @@ def test_canopy_division_domain_fallback_bit_exact(engines, oracle_port, perturb
     st = cols.state.copy()
     rng = np.random.default_rng(7)
     hit = np.arange(n) % 3 == 0
-    kinds = {"wind": [0], "pressure": [1], "fwet": [2], "mixed": [0, 1, 2]}[perturb]
+    kinds = {"wind": [0], "pressure": [1], "fwet": [2], "co2": [3], "eah": [4],
+             "mixed": [0, 1, 2, 3, 4]}[perturb]
     which = np.where(hit, rng.choice(kinds, n), -1)
     fi = L.FORCING.index
     f[fi("UU"), which == 0] = rng.uniform(150.0, 400.0, (which == 0).sum()).astype(np.float32)
     f[fi("SFCPRS"), which == 1] = np.float32(2.5e4)
     f[fi("PSFC"), which == 1] = np.float32(2.5e4)
     st[L.s("FWET").start, which == 2] = np.float32(1e-20)
+    # outside the stomata bisection's domain only (its divisions go IEEE)
+    f[fi("CO2AIR"), which == 3] = np.float32(0.5)
+    st[L.s("EAH").start, which == 4] = np.float32(1e-5)
     cols = dataclasses.replace(cols, state=st)
     cs = ColumnState.from_host(cols, DEV)
     diag = torch.zeros((L.NDIAG_FULL, n), device=DEV)

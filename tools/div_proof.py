@@ -122,6 +122,86 @@ def esat_range():
     return M(min(es), max(es)), M(min(des), max(des))
 
 
+def stomata_sites(D, T, p, es, rb):
+    """The stomata bisection's divisions (func.f90:3850-3879; sflx_kernel.hip
+    stomata_solve), per 1 K band of the canopy temperature TV: KC, KO, CP, AWC
+    and VCMX are functions of TV, so bounding them band by band keeps their
+    correlation (a hot canopy has a large KC and a small VCMX together).  Each
+    site's row is the worst case over the bands."""
+    RGAS, MPE = 8.314, 1e-6
+    box = lambda k: (D[k + "_LO"], D[k + "_HI"])
+    kc25, akc, ko25, ako, avcmx = box("KC25"), box("AKC"), box("KO25"), box("AKO"), box("AVCMX")
+    vcmx25, qe25, mp, bp = box("VCMX25"), box("QE25"), box("MP"), box("BP")
+    co2, o2 = M(*box("CO2")), M(*box("O2"))
+    apar, eah = M(*box("APAR")), M(D["EAH_LO"], D["EAH_HI"], True)
+    fnf = M(D["FNF_LO"], 1.0, True)
+    btran = M(MPE, 1.0001)                        # MAX(MPE, sum of root-layer shares)
+    cf = M(p.lo / (RGAS * T.hi) * 1e6, p.hi / (RGAS * T.lo) * 1e6)
+    rlb = M(rb.lo / cf.hi, rb.hi / cf.lo)         # RLB = RB / CF (IEEE, stomata_pre)
+    worst = {}
+
+    def pw(base, ex0, ex1):                       # base**ex over a box of bases and exponents
+        vals = [b ** e for b in base for e in (ex0, ex1)]
+        return min(vals), max(vals)
+
+    def g(t):                                      # the VCMX temperature factor's exponent
+        return (-2.2e5 + 710.0 * t) / (8.314 * t)
+
+    t_hi = D["STOMATA_TV_HI"]                    # checked before the calls
+    t0 = T.lo
+    while t0 < t_hi:
+        t1 = min(t0 + 1.0, t_hi)
+        ex0, ex1 = (t0 - TFRZ - 25.0) / 10.0, (t1 - TFRZ - 25.0) / 10.0
+        a_lo, a_hi = pw(akc, ex0, ex1)
+        kc = M(kc25[0] * a_lo, kc25[1] * a_hi)
+        o_lo, o_hi = pw(ako, ex0, ex1)
+        ko = M(ko25[0] * o_lo, ko25[1] * o_hi)
+        awc = M(kc.lo * (1 + o2.lo / ko.hi), kc.hi * (1 + o2.hi / ko.lo))
+        cp = M(0.105 * kc.lo * o2.lo / ko.hi, 0.105 * kc.hi * o2.hi / ko.lo)
+        v_lo, v_hi = pw(avcmx, ex0, ex1)
+        efac = M(1 + math.exp(g(t0)), 1 + math.exp(g(t1)))
+        vcmx = M(vcmx25[0] / efac.hi * fnf.lo * btran.lo * v_lo,
+                 vcmx25[1] / efac.lo * 1.0 * btran.hi * v_hi, True)
+        j = M(4.6 * apar.lo * qe25[0], 4.6 * apar.hi * qe25[1], True)
+        ci = M(1.5 * co2.lo * 2.0 ** -20, 1.5 * co2.hi)   # bisection midpoints of [0, 1.5 CO2]
+        dci = diff(ci, cp)                        # MAX(CI - CP, 0): 0 or >= granularity
+        rows_before = len(rows)
+        wj = site("stomata: WJ = (CI-CP)*J / (CI+2CP)", dci * j,
+                  M(ci.lo + 2 * cp.lo, ci.hi + 2 * cp.hi), ":3860")
+        wc = site("stomata: WC = (CI-CP)*VCMX / (CI+AWC)", dci * vcmx,
+                  M(ci.lo + awc.lo, ci.hi + awc.hi), ":3861")
+        we4 = site("stomata: WE = 4000*VCMX*CI / SFCPRS (C4)", 4000 * vcmx * ci, p, ":3866")
+        we3 = 0.5 * vcmx
+        lo = min(wj.lo, wc.lo, min(we3.lo, we4.lo))
+        hi = max(wj.hi, wc.hi, max(we3.hi, we4.hi))
+        psn = M(lo, hi, True)                     # MIN(WJ, WC, WE) * IGS, IGS = 0 or 1
+        cs = M(MPE, co2.hi)                       # MAX(CO2 - 1.37 RLB SFCPRS PSN, MPE)
+        num = M(mp[0], mp[1]) * psn * p
+        if t1 > D["TMIN_LO"]:
+            x = site("stomata: A = MP*PSN*SFCPRS*EA / (CS*EI)", num * eah, cs * es, ":3870",
+                     "EA = EAH, EI = ESTV; PSN > 0 needs TV > TMIN >= TMIN_LO")
+            xb = site("stomata: B = MP*PSN*SFCPRS / CS", num, cs, ":3871")
+        else:                                     # PSN = 0 (IGS = 0 or VCMX25 = 0): a = 0
+            x, xb = M(num.lo / cs.hi, num.hi / cs.lo), M(num.lo / cs.hi, num.hi / cs.lo)
+        a = M(bp[0], x.hi + bp[1])
+        bmag = M(1e-30, (xb.hi + bp[1]) * rlb.hi + 1.0, True)
+        q = M(math.sqrt(a.lo * rlb.lo), bmag.hi + math.sqrt(a.hi * rlb.hi))
+        site("stomata: R1 = Q / A", q, a, ":3875")
+        site("stomata: R2 = C / Q", rlb, q, ":3876", "C = -RLB")
+        for r in rows[rows_before:]:
+            name = r[0]
+            if name not in worst or not r[5] or (worst[name][5] and r[4].lo < worst[name][4].lo):
+                worst[name] = r
+        del rows[rows_before:]
+        t0 = t1
+    global bad
+    bad = [b for b in bad if not b.startswith("stomata:")]
+    for name, r in worst.items():
+        rows.append(r)
+        if not r[5]:
+            bad.append(name)
+
+
 def main():
     D = domain()
     # ---- loop-invariant inputs: the kernel's entry check (vege_domain.h) ----
@@ -254,6 +334,8 @@ def main():
     gammag = gammav                                  # same formula with LATHEAG
     cevi = site("bare: RHOAIR*CPAIR / GAMMA", rhocp, gammag, ":3187")
     site("bare: CEV = (...) / (RSURF+RAWB)", cevi, M(rahb.lo, rahb.hi + rsurf_hi), ":3187")
+
+    stomata_sites(D, T, p, es, rb)
 
     # ---- induction: the iteration ends inside the intervals it started from ----
     assert h_q.hi <= h.hi * 1.001 and h_q.lo >= h.lo * 0.999, (h_q, h)
