@@ -626,24 +626,27 @@ def test_cost_key_is_the_reference_trip_count(engines, oracle_port):
 _SINGLE_FIXTURES = ["single_" + n for n in single_names()]
 
 
+@pytest.mark.parametrize("precision", [4, 8])
 @pytest.mark.parametrize("variant", VARIANTS)
 @pytest.mark.parametrize("name", _SINGLE_FIXTURES)
-def test_diag_levels_consistent(engines, name, variant):
+def test_diag_levels_consistent(engines, name, variant, precision):
     """DIAG_OUT fields are the DIAG_FULL values (T2M = the fveg blend of
     T2MV/T2MB), and the state is the same bits at every diagnostics level --
     with no diagnostics the kernel skips the 2-m chain (MOZ2 -> FH2 -> CHV2,
     CHB2 -> T2M, Q2), which nothing else reads -- for every single-call
-    fixture (every option value and table pair), on both occupancy kernels."""
+    fixture (every option value and table pair), on both occupancy kernels,
+    in fp32 and fp64."""
     from noahmp_amd.engine import ColumnState
     g = load(name + ".npz")
-    eng = engines(g["options"], variant=variant)
+    eng = engines(g["options"], precision=precision, variant=variant)
+    dtype = torch.float32 if precision == 4 else torch.float64
     cols = cases.ColumnSet(g["static_f"], g["static_i"], g["state0"], g["isnow0"], *([None] * 7))
-    f = torch.as_tensor(g["forcing"], device=DEV).contiguous()
+    f = torch.as_tensor(g["forcing"], device=DEV).to(dtype).contiguous()
     outs = {}
     for lvl, nd in ((L.DIAG_FULL_LEVEL, L.NDIAG_FULL), (L.DIAG_OUT_LEVEL, L.NDIAG_OUT),
                     (L.DIAG_NONE, 0)):
-        cs = ColumnState.from_host(cols, DEV)
-        d = torch.zeros((max(nd, 1), cs.ncol), device=DEV) if nd else None
+        cs = ColumnState.from_host(cols, DEV, dtype)
+        d = torch.zeros((max(nd, 1), cs.ncol), dtype=dtype, device=DEV) if nd else None
         eng.step(cs, f, g["zsoil"], float(g["dt"]), float(g["julian"]), int(g["yearlen"]), d, lvl)
         torch.cuda.synchronize()
         outs[lvl] = (cs.state.cpu().numpy(), None if d is None else d.cpu().numpy())
@@ -651,7 +654,7 @@ def test_diag_levels_consistent(engines, name, variant):
     for i, n in enumerate(L.DIAG_OUT):
         if n != "T2M":
             np.testing.assert_array_equal(out[i], full[L.DIAG_FULL.index(n)], err_msg=n)
-    if name == "single_casenml_conus":
+    if name == "single_casenml_conus" and precision == 4:
         fveg = full[L.DIAG_FULL.index("FVEG")]
         t2m = out[L.DIAG_OUT.index("T2M")]
         veg = g["static_i"][L.STATIC_I.index("IST")] == 1
