@@ -323,7 +323,7 @@ DEV void sfcdif1(D& d, const Sfc1Inv<T>& inv, int iter, T h, const Sfc1Logs<T, R
   if (fabs(ch2fh2) <= mpe) ch2fh2 = mpe;
   cm = d.divk(KARMAN * KARMAN, d.rec(cmfm * cmfm));
   ch = d.divk(KARMAN * KARMAN, d.rec(cmfm * chfh));
-  fv = ur * M::sqrt(cm);
+  fv = ur * d.sqrt(cm);  // CM in the proof's interval (tools/div_proof.py)
 }
 
 // sfcdif2 (Chen97, opt_sfc=2): func.f90:3511-3689
@@ -421,7 +421,7 @@ DEV void ragrb(D& d, const Recip<T>& rhocp, const Recip<T>& rhcan, T dzg, T sqrt
   }
   T fhgnew = (mozg < L(0.0)) ? M::pow_mq(L(1.0) - L(15.0) * mozg) : L(1.0) + L(4.7) * mozg;
   fhg = (iter == 1) ? fhgnew : L(0.5) * (fhg + fhgnew);
-  T cwpc = M::sqrt(cwp * vai * hcan * fhg);
+  T cwpc = d.sqrt(cwp * vai * hcan * fhg);  // proven range (tools/div_proof.py)
   T tmp1 = M::exp(d.div(-cwpc * z0hg, rhcan));
   T tmp2 = M::exp(d.div(-cwpc * (z0h + zpd), rhcan));
   T tmprah2 = d.div(hcan * M::exp(cwpc), d.rec(cwpc)) * (tmp1 - tmp2);
@@ -500,8 +500,8 @@ DEV void stomata_solve(D& d, const VegRec& V, const StomataPre<T>& p, T igs, T s
     T a = d.div(mp * psn * sfcprs * ea, d.rec(cs * ei)) + bp;
     T b = (d.div(mp * psn * sfcprs, d.rec(cs)) + bp) * rlb - L(1.0);
     T c = -rlb;
-    T q = (b >= L(0.0)) ? L(-0.5) * (b + M::sqrt(b * b - L(4.0) * a * c))
-                        : L(-0.5) * (b - M::sqrt(b * b - L(4.0) * a * c));
+    T q = (b >= L(0.0)) ? L(-0.5) * (b + d.sqrt(b * b - L(4.0) * a * c))
+                        : L(-0.5) * (b - d.sqrt(b * b - L(4.0) * a * c));
     T r1 = d.div(q, d.rec(a));
     T r2 = d.div(c, d.rec(q));
     rs = rmax(r1, r2);

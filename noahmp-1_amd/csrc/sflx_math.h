@@ -155,6 +155,10 @@ __device__ __forceinline__ T p4(T x) { return x * p3(x); }
 template <class T>
 __device__ __forceinline__ T p5(T x) { return x * p4(x); }
 
+// NMP_SQRT_SHORT=0: the range-proven sqrt sites keep the IEEE lowering (A/B probe)
+#ifndef NMP_SQRT_SHORT
+#define NMP_SQRT_SHORT 1
+#endif
 // Division in the Newton loops (vege_flux, bare_flux, sfcdif1, ragrb).  fp32
 // (the bit-exact path): IEEE `/`, except at the range-proven sites that go
 // through DivFast32 (below).  fp64 (held to tolerances, not bits): the
@@ -259,7 +263,29 @@ struct DivRef {
   __device__ __forceinline__ T div(T a, const Recip<T>& R) const { return dv(a, R.b); }
   __device__ __forceinline__ T divk(T a, const Recip<T>& R) const { return dv(a, R.b); }
   __device__ __forceinline__ void chk(T) const {}
+  // the reference's SQRT: IEEE correctly rounded
+  __device__ __forceinline__ static T sqrt(T x) {
+    if constexpr (sizeof(T) == 4) return ::sqrtf(x);
+    else return ::sqrt(x);
+  }
 };
+
+// sqrt of a finite x >= 2^-96: the compiler's
+// correctly rounded fp32 sqrt sequence without its scaling of x < 2^-96 and
+// its zero / infinity / NaN select, neither of which changes a result in that
+// range.  v_sqrt_f32, then the two neighbour tests: s - 1 ulp if
+// fma(-(s-ulp), s, x) <= 0, s + 1 ulp if fma(-(s+ulp), s, x) > 0 -- the same
+// instructions in the same order as the IEEE lowering (tests/test_gpu_routines.py
+// compares it with sqrtf over the range).
+__device__ __forceinline__ float sqrt_normal32(float x) {
+  const float s = __builtin_amdgcn_sqrtf(x);
+  const float sm = __builtin_bit_cast(float, __builtin_bit_cast(uint32_t, s) - 1u);
+  const float vm = __builtin_fmaf(-sm, s, x);
+  float r = (vm <= 0.0f) ? sm : s;
+  const float sp = __builtin_bit_cast(float, __builtin_bit_cast(uint32_t, s) + 1u);
+  const float vp = __builtin_fmaf(-sp, s, x);
+  return (vp > 0.0f) ? sp : r;
+}
 
 // DivFast32: the short exact sequence, used where the operands are proven to
 // lie in its exact region (DESIGN.md "Division in the canopy loop").  The
@@ -299,6 +325,14 @@ struct DivFast32 {
 #endif
   __device__ __forceinline__ float divk(float a, const Recip<float>& R) const { return div(a, R); }
   __device__ __forceinline__ void chk(float) const {}
+  // at the range-proven sqrt sites (tools/div_proof.py): x finite and >= 2^-96
+  __device__ __forceinline__ static float sqrt(float x) {
+#if NMP_SQRT_SHORT
+    return sqrt_normal32(x);
+#else
+    return ::sqrtf(x);
+#endif
+  }
 };
 
 // Register-array access with a runtime index, lowered to a select chain so the

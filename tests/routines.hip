@@ -86,6 +86,14 @@ __global__ void k_dv64(int n, const double* a, const double* b, double* q, doubl
   ieee[i] = a[i] / b[i];
 }
 
+// the range-proven short sqrt (sflx_math.h sqrt_normal32) beside IEEE sqrtf
+__global__ void k_sqrt32(int n, const float* x, float* s, float* ieee) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  s[i] = nmp::sqrt_normal32(x[i]);
+  ieee[i] = ::sqrtf(x[i]);
+}
+
 // host helpers: device copies in, one launch, results out (synchronous)
 struct Dev {
   std::vector<void*> ptrs;
@@ -178,6 +186,17 @@ int rt_dv64(int n, const double* a, const double* b, double* q, double* ieee) {
   if (hipDeviceSynchronize() != hipSuccess) return -4;
   if (hipMemcpy(q, dq, n * sizeof(double), hipMemcpyDeviceToHost) != hipSuccess) return -4;
   return hipMemcpy(ieee, di, n * sizeof(double), hipMemcpyDeviceToHost) == hipSuccess ? 0 : -4;
+}
+
+int rt_sqrt32(int n, const float* x, float* s, float* ieee) {
+  Dev D;
+  const float* dx = D.in(x, n);
+  float *ds = D.in<float>(nullptr, n), *di = D.in<float>(nullptr, n);
+  if (!dx || !ds || !di) return -4;
+  hipLaunchKernelGGL(k_sqrt32, dim3((n + 255) / 256), dim3(256), 0, 0, n, dx, ds, di);
+  if (hipDeviceSynchronize() != hipSuccess) return -4;
+  if (hipMemcpy(s, ds, n * sizeof(float), hipMemcpyDeviceToHost) != hipSuccess) return -4;
+  return hipMemcpy(ieee, di, n * sizeof(float), hipMemcpyDeviceToHost) == hipSuccess ? 0 : -4;
 }
 
 }  // extern "C"

@@ -88,6 +88,7 @@ def rt():
     lib.rt_rosr12.argtypes = [C.c_int, i32p, f32p, f32p, f32p, f32p, f32p, f32p]
     f64p = np.ctypeslib.ndpointer(np.float64, flags="C_CONTIGUOUS")
     lib.rt_dv64.argtypes = [C.c_int, f64p, f64p, f64p, f64p]
+    lib.rt_sqrt32.argtypes = [C.c_int, f32p, f32p, f32p]
     return lib
 
 
@@ -399,3 +400,21 @@ def test_fortran_engine_slot_vs_reference(mode):
         ok = bit_equal(st, g["states"][s]).all(0) & bit_equal(dg, g["diags"][s]).all(0) & \
             (isn == g["isnows"][s]) & (as_ref_status(status) == g["statuses"][s])
         assert ok.all(), f"{mode}: step {s}: {int((~ok).sum())} of {n} columns differ"
+
+
+@pytest.mark.gpu
+def test_device_short_sqrt_equals_ieee_over_its_range(rt):
+    """sqrt_normal32 (csrc/sflx_math.h), used at the range-proven sqrt sites
+    (tools/div_proof.py), is IEEE sqrtf bit for bit for every finite x >= 2^-96:
+    every 13th float bit pattern of that range (about 1.4e8 values, 2^-96 up to
+    FLT_MAX, both ends included), checked against the device's IEEE sqrtf and
+    the host's."""
+    lo, hi = np.float32(2.0 ** -96).view(np.uint32), np.float32(3.4028235e38).view(np.uint32)
+    bits = np.arange(int(lo), int(hi) + 1, 13, dtype=np.uint64)
+    bits = np.concatenate([bits, [lo, hi, lo + 1, hi - 1]]).astype(np.uint32)
+    for chunk in np.array_split(bits, 16):
+        x = np.ascontiguousarray(chunk.view(np.float32))
+        s, ieee = np.empty_like(x), np.empty_like(x)
+        assert rt.rt_sqrt32(x.size, x, s, ieee) == 0
+        assert np.array_equal(s.view(np.uint32), ieee.view(np.uint32))
+        assert np.array_equal(ieee.view(np.uint32), np.sqrt(x).view(np.uint32))

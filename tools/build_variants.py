@@ -134,6 +134,7 @@ VARIANTS = {
     "no2mskip": ("-DNMP_SKIP_2M=0",),
     "gmbl": ("-DNMP_GM_BRANCHLESS=1",),
     "stfast": {"f32": ["-DNMP_STOMATA_FASTDIV"]},
+    "sqrtieee": {"f32": ["-DNMP_SQRT_SHORT=0"]},
     # round-4 re-sweep on the fp32 translation unit
     "bu1": {"f32": ["-DNMP_BARE_UNROLL=1"]},
     "bu3": {"f32": ["-DNMP_BARE_UNROLL=3"]},

@@ -102,6 +102,17 @@ def site(name, a, b, ref, note=""):
     return q
 
 
+def sqrt_site(name, x, ref, note=""):
+    """sqrt_normal32 (csrc/sflx_math.h) equals IEEE sqrtf for finite x >= 2^-96:
+    the IEEE lowering's own instructions minus its scaling of smaller x and
+    its zero / infinity / NaN select."""
+    ok = not x.z and 2.0 ** -96 <= x.lo and x.hi <= 3.4028234e38
+    rows.append((name, ref, x, M(1.0, 1.0), fn(math.sqrt, x), ok,
+                 ("sqrt: " + note) if note else "sqrt"))
+    if not ok:
+        bad.append(name)
+
+
 def esat_range():
     def poly(t, cs):
         v = 0.0
@@ -173,8 +184,11 @@ def stomata_sites(D, T, p, es, rb):
         we4 = site("stomata: WE = 4000*VCMX*CI / SFCPRS (C4)", 4000 * vcmx * ci, p, ":3866")
         we3 = 0.5 * vcmx
         lo = min(wj.lo, wc.lo, min(we3.lo, we4.lo))
-        hi = max(wj.hi, wc.hi, max(we3.hi, we4.hi))
-        psn = M(lo, hi, True)                     # MIN(WJ, WC, WE) * IGS, IGS = 0 or 1
+        # PSN = MIN(WJ, WC, WE) * IGS (IGS = 0 or 1) <= MIN(J, VCMX): WJ <= J and
+        # WC <= VCMX because (CI-CP) < CI+2CP and < CI+AWC (C3); WJ = J, WC =
+        # VCMX (C4) -- a bound interval arithmetic on the quotients loses
+        hi = min(j.hi, vcmx.hi)
+        psn = M(lo, hi, True)
         cs = M(MPE, co2.hi)                       # MAX(CO2 - 1.37 RLB SFCPRS PSN, MPE)
         num = M(mp[0], mp[1]) * psn * p
         if t1 > D["TMIN_LO"]:
@@ -185,6 +199,8 @@ def stomata_sites(D, T, p, es, rb):
             x, xb = M(num.lo / cs.hi, num.hi / cs.lo), M(num.lo / cs.hi, num.hi / cs.lo)
         a = M(bp[0], x.hi + bp[1])
         bmag = M(1e-30, (xb.hi + bp[1]) * rlb.hi + 1.0, True)
+        sqrt_site("stomata: SQRT(B*B - 4*A*C)", M(4 * a.lo * rlb.lo, bmag.hi ** 2 + 4 * a.hi * rlb.hi),
+                  ":3873", "C = -RLB < 0, so the radicand is >= 4*A*RLB")
         q = M(math.sqrt(a.lo * rlb.lo), bmag.hi + math.sqrt(a.hi * rlb.hi))
         site("stomata: R1 = Q / A", q, a, ":3875")
         site("stomata: R2 = C / Q", rlb, q, ":3876", "C = -RLB")
@@ -254,6 +270,7 @@ def main():
                 "CMFM >= 0.1 TMPCM: FM <= 0.9 TMPCM (:3455)")
     site("CH = KARMAN**2 / (CMFM*CHFH)", c(0.16), cmfm * cmfm, ":3500")
     assert cm_q.lo >= cm.lo * (1 - 1e-4) and cm_q.hi <= cm.hi * (1 + 1e-4)
+    sqrt_site("FV = UR*SQRT(CM)", cm, ":3502", "also bare_flux's sfcdif1")
     # ---- vege_flux: canopy resistance, :2775 ----
     site("RAHC: 1 / (CH*UR)", c(1.0), cm * ur, ":2775", "then MAX(1, .)")
     # ---- ragrb (iter >= 2), :3301-3306 ----
@@ -266,6 +283,7 @@ def main():
     mozg = site("MOZG = (ZPD-Z0MG) / MOLG", dzg, molg, ":3316", "then MIN(., 1)")
     fhg_lo = (1.0 + 15.0 * mozg.hi) ** -0.25        # (1 - 15 MOZG)**-0.25, MOZG < 0
     fhg = M(fhg_lo, 5.7)                            # 1 + 4.7 MOZG <= 5.7; averages stay inside
+    sqrt_site("CWPC = SQRT(CWP*VAI*HCAN*FHG)", cwph * fhg, ":3343")
     cwpc = fn(math.sqrt, cwph * fhg)                # SQRT(CWP*VAI*HCAN*FHG)
     a14 = cwpc * z0
     q14 = site("CWPC*Z0HG / HCAN", a14, hcan, ":3334", "Z0MG <= HCAN checked: <= CWPC")
@@ -344,7 +362,8 @@ def main():
     assert p.lo - 0.378 * eah.hi > 0
 
     print(f"domain: {HDR}")
-    print(f"exact region: |b| in [2^-126, 2^126], a = 0 or |a| >= 2^-102, |a/b| in [2^-126, 2^126]")
+    print(f"exact region: |b| in [2^-126, 2^126], a = 0 or |a| >= 2^-102, |a/b| in [2^-126, 2^126]; "
+          f"sqrt: x finite and >= 2^-96")
     print(f"{'site':46s} {'func.f90':8s} {'|a|':>22s} {'|b|':>22s} {'|a/b|':>22s}  ok")
     for name, ref, a, b, q, ok, note in rows:
         print(f"{name:46s} {ref:8s} {a!r:>22s} {b!r:>22s} {q!r:>22s}  {'yes' if ok else 'NO'}"
