@@ -44,7 +44,11 @@
  *    in col_status instead; the column continues, as the reference code does
  *    after the external returns.
  *  - Threading: one engine per device; calls on one engine are serialised by
- *    the caller.  Engines on different devices/ranks are independent.
+ *    the caller.  Engines on different devices/ranks are independent.  The
+ *    synchronous host entries (nmp_sflx_columns, nmp_frh2o_host,
+ *    nmp_calhum_host) share one device scratch block and stream per engine
+ *    and take an engine lock, so concurrent calls of them are safe (they run
+ *    one after another).
  */
 #ifndef NOAHMP_ENGINE_H
 #define NOAHMP_ENGINE_H

@@ -11,6 +11,7 @@
 #include <cstdint>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <new>
 #include <vector>
 
@@ -36,6 +37,9 @@ struct nmp_engine {
   hipStream_t hstream;
   char* scratch;
   size_t scratch_bytes;
+  // the host entries share hstream and scratch: one at a time per engine
+  // (two threads calling them on one engine are serialized here)
+  std::mutex host_mu;
 };
 
 namespace {
@@ -590,14 +594,16 @@ int sflx_columns(nmp_engine* eng, nmp_sflx_args* cols, int64_t n) {
   const auto down = [&](void* dst, const void* src, size_t nb) {
     return hipMemcpyAsync(dst, src, nb, hipMemcpyDeviceToHost, hs) == hipSuccess;
   };
+  int rc = NMP_OK;
   if (!(up(d_st, h.st.data(), nb_st) && up(d_sf, h.sf.data(), nb_sf) &&
         up(d_fc, h.fc.data(), nb_fc) && up(d_fo, h.fo.data(), nb_fo) &&
         up(d_isn, h.isn.data(), nb_i) && up(d_si, h.si.data(), nb_i * NMP_NSTATIC_I) &&
         hipMemsetAsync(d_status, 0, nb_i, hs) == hipSuccess &&
         hipMemsetAsync(d_dg, 0, nb_dg, hs) == hipSuccess))
-    return NMP_E_DEVICE;
-  int rc = launch(eng, n, n, r0.zsoil, r0.dt, r0.julian, r0.yearlen, d_st, d_isn, d_sf, d_si, d_fc,
-                  d_dg, NMP_DIAG_FULL, d_status, hs, nullptr, nullptr, d_fo);
+    rc = NMP_E_DEVICE;  // (copies already queued are drained below before `h` goes)
+  if (rc == NMP_OK)
+    rc = launch(eng, n, n, r0.zsoil, r0.dt, r0.julian, r0.yearlen, d_st, d_isn, d_sf, d_si, d_fc,
+                d_dg, NMP_DIAG_FULL, d_status, hs, nullptr, nullptr, d_fo);
   if (rc == NMP_OK && !(down(h.st.data(), d_st, nb_st) && down(h.dg.data(), d_dg, nb_dg) &&
                         down(h.isn.data(), d_isn, nb_i) && down(h.status.data(), d_status, nb_i)))
     rc = NMP_E_DEVICE;
@@ -617,6 +623,7 @@ int nmp_sflx_columns(nmp_engine* eng, nmp_sflx_args* cols, int64_t n) {
   if (!eng || n < 0 || (n > 0 && !cols)) return NMP_E_ARG;
   if (n == 0) return NMP_OK;
   if (ensure_device(eng->device) != NMP_OK) return NMP_E_DEVICE;
+  std::lock_guard<std::mutex> lk(eng->host_mu);
   return eng->precision == 4 ? sflx_columns<float>(eng, cols, n)
                              : sflx_columns<double>(eng, cols, n);
 }
@@ -655,6 +662,7 @@ int nmp_frh2o_host(nmp_engine* eng, int64_t n, const int32_t* sltyp, const void*
   if (!sltyp || !tkelv || !smc || !soilwat || !free_water) return NMP_E_ARG;
   if (ensure_device(eng->device) != NMP_OK) return NMP_E_DEVICE;
   const size_t nr = (size_t)n * eng->precision, ni = (size_t)n * sizeof(int32_t);
+  std::lock_guard<std::mutex> lk(eng->host_mu);
   char* base = host_scratch(eng, 4 * nr + 2 * ni);
   if (!base) return NMP_E_DEVICE;
   char *t = base, *m = t + nr, *w = m + nr, *o = w + nr;
@@ -685,6 +693,7 @@ int nmp_calhum_host(nmp_engine* eng, int64_t n, const void* sfctmp, const void* 
   if (!sfctmp || !sfcprs) return NMP_E_ARG;
   if (ensure_device(eng->device) != NMP_OK) return NMP_E_DEVICE;
   const size_t nr = (size_t)n * eng->precision;
+  std::lock_guard<std::mutex> lk(eng->host_mu);
   char* base = host_scratch(eng, 4 * nr);
   if (!base) return NMP_E_DEVICE;
   char *t = base, *p = t + nr, *q = p + nr, *dq = q + nr;

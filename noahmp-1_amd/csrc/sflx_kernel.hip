@@ -1573,14 +1573,13 @@ DEV void sflx_column(const DevParams& P, const KArgs<T>& A, Col<T>& c, const Sin
         c.qsfc = d.div(L(0.622) * c.eah, d.rec(c.sfcprs - L(0.378) * c.eah));
         return dtv;
       };
-      auto tv_in_window = [&]() { return in(c.tv, (T)NMP_DOM_T_LO, (T)NMP_DOM_T_HI); };
-      if constexpr (kFast) NMP_DOM(ok, 18, tv_in_window());
+      if constexpr (kFast) NMP_DOM(ok, 18, in(c.tv, (T)NMP_DOM_T_LO, (T)NMP_DOM_T_HI));
       vtrips = 1;
       vege_iter(1, std::true_type{});  // iter 1 cannot exit (the test needs iter >= 5)
       NMP_UNROLL(NMP_VEGE_UNROLL)
       for (int iter = 2; iter <= 20; ++iter) {
         vtrips = iter;
-        if constexpr (kFast) NMP_DOM(ok, 19, tv_in_window());
+        if constexpr (kFast) NMP_DOM(ok, 19, in(c.tv, (T)NMP_DOM_T_LO, (T)NMP_DOM_TV_HI));
         const T dtv = vege_iter(iter, std::false_type{});
         if (liter == 1) break;
         if (iter >= 5 && fabs(dtv) <= L(0.01) && liter == 0) liter = 1;
@@ -1701,7 +1700,7 @@ NMP_UNROLL(NMP_LOOP2_UNROLL)
       const Sfc1Inv<T> invb = sfc1_inv(d, c.sfctmp, qair, rhoair, zlvl, zpdg, z0h);
 NMP_UNROLL(NMP_BARE_UNROLL)
       for (int iter = 1; iter <= 5; ++iter) {
-        if constexpr (kFast) NMP_DOM(ok, 20, in(tgb, (T)NMP_DOM_T_LO, (T)NMP_DOM_T_HI));
+        if constexpr (kFast) NMP_DOM(ok, 20, in(tgb, (T)NMP_DOM_T_LO, (T)NMP_DOM_TGB_HI));
         if (o.sfc == 1)
           sfcdif1<T, R>(d, invb, iter, h, lgb, ur, mpe, moz, mozsgn, fm, fh, fm2, fh2, cmb, chb, fv,
                         diag_on);

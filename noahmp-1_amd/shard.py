@@ -77,7 +77,12 @@ class DiagGather:
     (gloo moves host tensors); the staging is synchronous."""
 
     def __init__(self, nfield: int, ncol_total: int, dtype, device, dst: int | None = 0,
-                 nbuf: int = 2, group=None, comm: torch.cuda.Stream | None = None):
+                 nbuf: int = 2, group=None, comm: torch.cuda.Stream | None = None,
+                 force_collective: bool = False):
+        """force_collective: issue the collective even on a single rank (where
+        nothing needs to move), so the RCCL code path of a multi-GPU run can
+        be executed and checked on one GPU (tests/probe_rccl_gather.py)."""
+        self.force_collective = bool(force_collective)
         self.group = group
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
@@ -112,7 +117,7 @@ class DiagGather:
         already holds its block in its slot: nothing moves, no collective runs
         (an in-place self-gather of 64 MB under RCCL cost 4 % of the N = 1
         bench, the collective's kernel taking CUs from the step)."""
-        if self.world == 1:
+        if self.world == 1 and not self.force_collective:
             self.local_producers[b] = list(producers)  # assemble() waits for them
             return
         bufs = self.host if self.staged else self.bufs

@@ -9,6 +9,8 @@
 //   frh2o  func.f90:4494-4598   supercooled soil water (Newton + Flerchinger)
 //   rosr12 func.f90:4240-4288   tridiagonal (Thomas) solve on layers kt..6
 //   dv     the fp64 Newton-loop division (csrc/sflx_math.h), against IEEE `/`
+//   sqrt_normal32 / DivFast32: the short fp32 sqrt and division of the
+//          range-proven sites, exhaustively / at the edges of their exact region
 // tests/test_gpu_routines.py compares them bit for bit with the oracle's C
 // restatement of each routine, and frh2o also with the reference's own
 // (public) frh2o.  Built by __graft_entry__.build() into tests/lib/.
@@ -92,6 +94,62 @@ __global__ void k_sqrt32(int n, const float* x, float* s, float* ieee) {
   if (i >= n) return;
   s[i] = nmp::sqrt_normal32(x[i]);
   ieee[i] = ::sqrtf(x[i]);
+}
+
+// Exhaustive sqrt check: every bit pattern u in [lo, hi] (a grid-stride loop),
+// sqrt_normal32 against the device's IEEE sqrtf and against the double square
+// root rounded to float (correctly rounded: 53 >= 2*24 + 2 bits).  Mismatches
+// are counted per thread and added once; the smallest mismatching pattern is
+// kept.
+__global__ void k_sqrt32_all(unsigned lo, unsigned hi, unsigned long long* bad, unsigned* first) {
+  const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t nthr = (uint64_t)gridDim.x * blockDim.x;
+  unsigned long long n = 0;
+  for (uint64_t u = lo + tid; u <= hi; u += nthr) {
+    const float x = __uint_as_float((unsigned)u);
+    const unsigned s = __float_as_uint(nmp::sqrt_normal32(x));
+    const unsigned w = __float_as_uint(::sqrtf(x));
+    const unsigned d = __float_as_uint((float)::sqrt((double)x));
+    if (s != w || s != d) {
+      ++n;
+      atomicMin(first, (unsigned)u);
+    }
+  }
+  if (n) atomicAdd(bad, n);
+}
+
+// DivFast32 at the edges of its exact region (sflx_math.h: b normal with a
+// normal reciprocal, a = 0 or |a| >= 2^-102, quotient normal).  Operands
+// a = +-(1 + ia/2^23) 2^ea, b = (1 + ib/2^23) 2^eb for ia over [0, 2^23) in
+// steps of sa and ib over [0, 2^23) in steps of sb (offsets oa, ob); pairs
+// whose IEEE quotient is not normal are outside the region and skipped.  Each
+// thread takes one ib value and a chunk of 2^14 consecutive ia steps.
+// cnt[0] pairs checked, cnt[1] mismatches (short sequence vs IEEE a/b).
+constexpr unsigned kDivChunk = 1u << 14;
+__global__ void k_div32_edge(int ea, int eb, unsigned sa, unsigned oa, unsigned sb, unsigned ob,
+                             unsigned nchunk, unsigned long long* cnt, unsigned* first) {
+  const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t ib = ob + (k / nchunk) * (uint64_t)sb;
+  if (ib >= (1u << 23)) return;
+  const float b = ldexpf(__uint_as_float(0x3f800000u | (unsigned)ib), eb);
+  const nmp::DivFast32 d;
+  const nmp::Recip<float> R = d.rec(b);
+  unsigned long long n = 0, nb = 0;
+  const uint64_t i0 = oa + (k % nchunk) * (uint64_t)kDivChunk * sa;
+  for (uint64_t j = 0, ia = i0; j < kDivChunk && ia < (1u << 23); ++j, ia += sa) {
+    const float m = __uint_as_float(0x3f800000u | (unsigned)ia);
+    const float a = ldexpf((ia & 1) ? -m : m, ea);
+    const float w = a / b;
+    const float aw = fabsf(w);
+    if (!(aw >= 0x1p-126f && aw <= 3.40282347e38f)) continue;
+    ++n;
+    if (__float_as_uint(d.div(a, R)) != __float_as_uint(w)) {
+      ++nb;
+      atomicMin(first, (unsigned)ib);
+    }
+  }
+  if (n) atomicAdd(&cnt[0], n);
+  if (nb) atomicAdd(&cnt[1], nb);
 }
 
 // host helpers: device copies in, one launch, results out (synchronous)
@@ -197,6 +255,47 @@ int rt_sqrt32(int n, const float* x, float* s, float* ieee) {
   if (hipDeviceSynchronize() != hipSuccess) return -4;
   if (hipMemcpy(s, ds, n * sizeof(float), hipMemcpyDeviceToHost) != hipSuccess) return -4;
   return hipMemcpy(ieee, di, n * sizeof(float), hipMemcpyDeviceToHost) == hipSuccess ? 0 : -4;
+}
+
+// mismatches of sqrt_normal32 over every bit pattern in [lo, hi]; *first = the
+// smallest mismatching pattern (0xffffffff if none)
+int rt_sqrt32_all(unsigned lo, unsigned hi, unsigned long long* bad, unsigned* first) {
+  Dev D;
+  unsigned long long* db = D.in<unsigned long long>(nullptr, 1);
+  unsigned* df = D.in<unsigned>(nullptr, 1);
+  if (!db || !df) return -4;
+  const unsigned none = 0xffffffffu;
+  if (hipMemset(db, 0, sizeof(*db)) != hipSuccess ||
+      hipMemcpy(df, &none, sizeof(none), hipMemcpyHostToDevice) != hipSuccess)
+    return -4;
+  hipLaunchKernelGGL(k_sqrt32_all, dim3(65536), dim3(256), 0, 0, lo, hi, db, df);
+  if (hipDeviceSynchronize() != hipSuccess) return -4;
+  if (hipMemcpy(bad, db, sizeof(*db), hipMemcpyDeviceToHost) != hipSuccess) return -4;
+  return hipMemcpy(first, df, sizeof(*df), hipMemcpyDeviceToHost) == hipSuccess ? 0 : -4;
+}
+
+// DivFast32 vs IEEE division on one exponent pair (k_div32_edge); cnt2 =
+// {pairs checked, mismatches}
+int rt_div32_edge(int ea, int eb, unsigned sa, unsigned oa, unsigned sb, unsigned ob,
+                  unsigned long long* cnt2, unsigned* first) {
+  if (sa == 0 || sb == 0 || oa >= sa || ob >= sb) return -1;
+  Dev D;
+  unsigned long long* dc = D.in<unsigned long long>(nullptr, 2);
+  unsigned* df = D.in<unsigned>(nullptr, 1);
+  if (!dc || !df) return -4;
+  const unsigned none = 0xffffffffu;
+  if (hipMemset(dc, 0, 2 * sizeof(*dc)) != hipSuccess ||
+      hipMemcpy(df, &none, sizeof(none), hipMemcpyHostToDevice) != hipSuccess)
+    return -4;
+  const uint64_t nbv = ((1u << 23) - ob + sb - 1) / sb;               // b values
+  const uint64_t nav = ((1u << 23) - oa + sa - 1) / sa;               // a values
+  const unsigned nchunk = (unsigned)((nav + kDivChunk - 1) / kDivChunk);
+  const uint64_t nthr = nbv * nchunk;
+  hipLaunchKernelGGL(k_div32_edge, dim3((unsigned)((nthr + 255) / 256)), dim3(256), 0, 0, ea, eb,
+                     sa, oa, sb, ob, nchunk, dc, df);
+  if (hipDeviceSynchronize() != hipSuccess) return -4;
+  if (hipMemcpy(cnt2, dc, 2 * sizeof(*dc), hipMemcpyDeviceToHost) != hipSuccess) return -4;
+  return hipMemcpy(first, df, sizeof(*df), hipMemcpyDeviceToHost) == hipSuccess ? 0 : -4;
 }
 
 }  // extern "C"

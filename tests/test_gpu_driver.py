@@ -285,3 +285,25 @@ def test_driver_device_forcing_independent_of_world_size(engine_lib, tmp_path):
                        nprocs=2, start_method="spawn")
     got = np.concatenate([np.load(tmp_path / f"dev{r}.npz")["state"] for r in range(2)], axis=1)
     assert bit_equal(got, ref).all()
+
+
+def test_rccl_gather_path_on_one_gpu(engine_lib):
+    """the RCCL branch of the diagnostics gather
+    (DiagGather._issue -> all_gather_into_tensor / gather to a root, and
+    gather_diag's nccl branches) executed on a world-1 "nccl" group with
+    force_collective, inside the bench's double-buffered output loop on a
+    comm side stream: every assembled output step equals the plain run's
+    diagnostics bit for bit (tests/probe_rccl_gather.py, in a child process
+    because it creates a process group)."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, os.path.join(root, "tests", "probe_rccl_gather.py")],
+                       capture_output=True, text=True, timeout=110,
+                       env=dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0"))
+    line = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert line, f"probe produced no result (rc {r.returncode}): {r.stderr[-3000:]}"
+    res = json.loads(line[-1])
+    print(res)
+    assert r.returncode == 0 and res["ok"], res

@@ -89,6 +89,10 @@ def rt():
     f64p = np.ctypeslib.ndpointer(np.float64, flags="C_CONTIGUOUS")
     lib.rt_dv64.argtypes = [C.c_int, f64p, f64p, f64p, f64p]
     lib.rt_sqrt32.argtypes = [C.c_int, f32p, f32p, f32p]
+    u64p, u32p = C.POINTER(C.c_ulonglong), C.POINTER(C.c_uint)
+    lib.rt_sqrt32_all.argtypes = [C.c_uint, C.c_uint, u64p, u32p]
+    lib.rt_div32_edge.argtypes = [C.c_int, C.c_int, C.c_uint, C.c_uint, C.c_uint, C.c_uint,
+                                  u64p, u32p]
     return lib
 
 
@@ -418,3 +422,53 @@ def test_device_short_sqrt_equals_ieee_over_its_range(rt):
         assert rt.rt_sqrt32(x.size, x, s, ieee) == 0
         assert np.array_equal(s.view(np.uint32), ieee.view(np.uint32))
         assert np.array_equal(ieee.view(np.uint32), np.sqrt(x).view(np.uint32))
+
+
+@pytest.mark.gpu
+def test_device_short_sqrt_exhaustive(rt):
+    """the short sqrt's claim (sqrt_normal32 == IEEE sqrtf
+    for every finite x >= 2^-96) checked on EVERY float bit pattern of that
+    range, 2^-96 .. FLT_MAX (1.87e9 patterns), on the device against its IEEE
+    sqrtf and against the double square root rounded to float: 0 mismatches."""
+    lo = int(np.float32(2.0 ** -96).view(np.uint32))
+    hi = int(np.float32(3.4028235e38).view(np.uint32))
+    bad, first = C.c_ulonglong(), C.c_uint()
+    assert rt.rt_sqrt32_all(lo, hi, C.byref(bad), C.byref(first)) == 0
+    print(f"sqrt_normal32: {hi - lo + 1} patterns, {bad.value} mismatches")
+    assert bad.value == 0, f"first mismatching pattern {first.value:#010x}"
+    # below the range the short form is not claimed (the compiler's scaling of
+    # x < 2^-96 is skipped): reported only
+    bad2 = C.c_ulonglong()
+    assert rt.rt_sqrt32_all(1, lo - 1, C.byref(bad2), C.byref(first)) == 0
+    print(f"  (below 2^-96, not claimed: {bad2.value} of {lo - 1} patterns differ)")
+
+
+# Exponent pairs (ea, eb) at the edges of DivFast32's exact region: |a| at its
+# smallest exponent (-102) over b near 1 and large; b at the smallest normal
+# exponent (-126, reciprocal near 2^126) and at the largest with a normal
+# reciprocal (125); quotients at the bottom (2^-126) and top (2^127) of the
+# normal range; and the interior reference pair (0, 0).
+DIV_EDGES = [(-102, 0), (-102, -1), (-102, 23), (-102, -126), (0, -126), (1, -126), (-60, -126),
+             (127, 125), (0, 125), (-1, 125), (126, 0), (127, 0), (127, -1), (-126 + 24, 24),
+             (0, 0)]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ea,eb", DIV_EDGES)
+def test_device_fast_division_at_region_edges(rt, ea, eb):
+    """DivFast32 (sflx_math.h) against IEEE a/b at the
+    exponent edges of its exact region.  For each exponent pair: every a
+    significand (2^23, both signs alternating) against 1,024 b significands
+    (every 8,192nd, offset 4,097) and every b significand against 1,024 a
+    significands: 1.7e10 pairs per edge; pairs whose IEEE quotient is not
+    normal are outside the region and skipped.  0 mismatches."""
+    tot = [0, 0]
+    for sa, oa, sb, ob in ((1, 0, 8192, 4097), (8192, 4097, 1, 0)):
+        cnt, first = (C.c_ulonglong * 2)(), C.c_uint()
+        assert rt.rt_div32_edge(ea, eb, sa, oa, sb, ob, cnt, C.byref(first)) == 0
+        tot[0] += cnt[0]
+        tot[1] += cnt[1]
+        assert cnt[1] == 0, f"(ea, eb) = ({ea}, {eb}): {cnt[1]} mismatches, first b " \
+                            f"significand {first.value}"
+    print(f"DivFast32 at (2^{ea}, 2^{eb}): {tot[0]} pairs in the region, {tot[1]} mismatches")
+    assert tot[0] > 0

@@ -294,7 +294,10 @@ def main():
     tmp1e = M(math.exp(-q14.hi), 1.0)
     tmp2e = M(math.exp(-q15.hi), 1.0)
     rah2a = site("HCAN*EXP(CWPC) / CWPC", hcan * fn(math.exp, cwpc), cwpc, ":3336")
-    # TMP1 >= TMP2 (Z0MG <= Z0M + ZPD checked); their difference is 0 or >= granularity
+    # |TMP1 - TMP2|: the sign is not assumed (the kernel does not check
+    # Z0MG <= Z0M + ZPD).  Nonzero, the difference is at least the granularity
+    # of the smaller exponential; a negative RAHG fails the RAHG window below
+    # and the lane re-runs with IEEE division.
     dtmp = M(2.0 ** (math.floor(math.log2(tmp2e.lo)) - 23), 1.0, True)
     kh = M(1e-6, KARMAN * fv.hi * D["HCAN_HI"])    # MAX(KARMAN*FV*(HCAN-ZPD), MPE)
     site("RAHG = TMPRAH2 / KH", rah2a * dtmp, kh, ":3341", "then checked in [RAHG_LO, RAHG_HI]")
