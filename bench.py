@@ -80,6 +80,12 @@ def valu_weighted(tj: dict, launches: int, step_ms: float):
         # exceed the SIMDs' cycles -- reported raw, not as a pipe share
         out["active_inst_valu_per_simd_cycle"] = (4 * tj["SQ_ACTIVE_INST_VALU"] * launches
                                                   / avail)
+    if "lane_util" in tj:
+        # share of the 64 lanes doing useful work in the VALU cycles the waves
+        # issue (SQ_THREAD_CYCLES_VALU / (64 SQ_ACTIVE_INST_VALU), one PMC pass):
+        # masked-off lanes (divergence, Newton loops running their wave's
+        # slowest lane) are the difference to 1
+        out["lane_util"] = tj["lane_util"]
     return out
 METRIC = BASELINE_METRIC = "land-columns·timesteps/sec at 4 soil + 3 snow layers, 1/2/4/8 MI355X"
 
@@ -161,6 +167,15 @@ def parse():
                     help="launcher check only (CPU tests): every rank joins the process group "
                          "over gloo and contributes its column count, rank 0 prints the line "
                          "with n_gpus and the summed columns; no GPU is touched, no rate")
+    ap.add_argument("--vege-cap", type=int, default=None,
+                    help="cap and resume of the canopy Newton loop at this many iterations "
+                         "(nmp_set_vege_cap: 2..19, 0 = off; default: the engine's)")
+    ap.add_argument("--launch-cols", type=int, default=0,
+                    help="(launch-size study) step each stream's column range as sequential "
+                         "launches of at most this many columns (0 = one launch per range)")
+    ap.add_argument("--replicate", type=int, default=1,
+                    help="(launch-size study) generate ncol/R columns, order them, and tile "
+                         "the ordered set R times: the waves of a small set in a large launch")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic.json"),
                     help="PMC-measured HBM bytes per launch (written by tools/pmc_traffic.py)")
     return ap.parse_args()
@@ -299,12 +314,16 @@ def main():
     opt_dict = dict(L.CASE_NML_OPTIONS, opt_veg=a.opt_veg)
     options = L.options_tuple(opt_dict)
     julian0, yearlen, seed = 180.0, 366, 1000 + rank
-    cols = cases.make_columns(a.ncol, a.kind, pdict, seed=seed, julian=julian0,
+    assert a.replicate >= 1 and a.ncol % a.replicate == 0
+    ngen = a.ncol // a.replicate
+    cols = cases.make_columns(ngen, a.kind, pdict, seed=seed, julian=julian0,
                               first=rank * a.ncol)
     if a.order != "as-generated":
         from noahmp_amd.order import coherent_order
         cols = cols.take(coherent_order(cols.lon, cols.static_i, cols.isnow, a.order,
                                         band_deg=a.order_band))
+    if a.replicate > 1:
+        cols = cols.take(np.tile(np.arange(ngen), a.replicate))
 
     # ---- CPU baseline (rank 0, N=1), BEFORE anything touches the GPU ------
     cpu = None
@@ -332,6 +351,8 @@ def main():
     dtype = torch.float32 if a.precision == 4 else torch.float64
     eng = Engine(P, opt_dict, device=local, precision=a.precision, math=a.math)
     eng.set_cols_per_wave(a.cpw)
+    if a.vege_cap is not None:
+        eng.vege_cap(a.vege_cap)
     from noahmp_amd import lib as _nlib
     build_hash = _nlib.load().nmp_build_hash().decode()  # lib.load refuses a stale library
     cs = ColumnState.from_host(cols, dev, dtype)
@@ -347,7 +368,8 @@ def main():
         F = torch.empty((2, L.NFORCING, n), dtype=dtype, device=dev)
         clim = torch.as_tensor(cases.climate(cols), device=dev).to(dtype).contiguous()
     gather_dst = 0 if a.gather == "root" else None
-    ranges = StreamShards(eng, cs, a.streams, rebin_tile=a.rebin_tile, rebin_every=a.rebin_every)
+    ranges = StreamShards(eng, cs, a.streams, rebin_tile=a.rebin_tile, rebin_every=a.rebin_every,
+                          launch_cols=a.launch_cols)
     comm = torch.cuda.Stream(dev) if use_dist else None
     if use_dist:
         # after the range streams exist: RCCL's communicator creates streams of
@@ -460,6 +482,7 @@ def main():
                        "ncol_total": world * n, "dt_s": a.dt, "out_every": a.out_every,
                        "math": a.math, "column_order": a.order, "forcing": a.forcing,
                        "streams": len(ranges.ranges), "cols_per_wave": a.cpw or "auto",
+                       "vege_cap": eng.vege_cap(),
                        "rebin": {"tile": a.rebin_tile, "every": a.rebin_every}
                        if a.rebin_tile else None,
                        "parallelism": f"column-shard x{world}",

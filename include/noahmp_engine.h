@@ -25,7 +25,7 @@
  * nmp_state_from_aos          layout bridge from noahmp_state_t records
  *                                                           core/module_noahmp_type.f90:10-42
  * nmp_finalize, nmp_strerror  (error path of utils `assert`/`stop`, core/module_noahmp_utils.f90:21-53)
- * nmp_set_launch_variant, nmp_type_size, nmp_option_set, nmp_set_math,
+ * nmp_set_launch_variant, nmp_set_vege_cap, nmp_type_size, nmp_option_set, nmp_set_math,
  *   nmp_set_cols_per_wave     engine tuning / host layout checks (no reference counterpart)
  *
  * Conventions
@@ -38,7 +38,8 @@
  *    in the reference (real(r4) module arrays).
  *  - Pointers passed to nmp_step are DEVICE pointers on the engine's device;
  *    `stream` is a hipStream_t (NULL = default stream).  nmp_step only
- *    enqueues work; it never synchronises and never allocates.
+ *    enqueues work; it never synchronises, and allocates only the per-stream
+ *    side buffer of nmp_set_vege_cap, stream-ordered, at first use.
  *  - Return codes: 0 ok, negative = NMP_E_*.  Per-column physics failures
  *    that abort the reference (wrf_error_fatal) are reported as NMP_ST_* bits
  *    in col_status instead; the column continues, as the reference code does
@@ -60,7 +61,7 @@
 extern "C" {
 #endif
 
-#define NMP_ABI_VERSION 5
+#define NMP_ABI_VERSION 6
 
 /* ---- dimensions (core/module_noahmp_global.f90:9-13) -------------------- */
 #define NMP_NSOIL 4
@@ -415,6 +416,19 @@ int nmp_option_set(nmp_engine* eng, int request);
  * the default at nmp_init.  Returns the variant in use, or NMP_E_ARG;
  * request -1 only queries.  Results do not depend on it.  The fp32 "fast"
  * math kernel has one instantiation (full) and ignores the setting. */
+/* Cap and resume of the canopy Newton loop (vege_flux, func.f90:2744-2877).
+ * The loop runs until its own exit test, up to 20 iterations, and a wave runs
+ * its slowest lane.  With k > 0, a production-size fp32 launch (compiled
+ * option set, "ref" math, full occupancy) stops every lane still iterating
+ * after k iterations, saves its loop context to a per-stream side buffer and
+ * finishes those columns -- the remaining iterations and the rest of the step
+ * -- in a second, compacted launch on the same stream.  Results are the same
+ * bits either way (DESIGN.md "Cap and resume").  k: 2..19, 0 = off, -1 =
+ * query.  Env NMP_VEGE_CAP=k sets the default at nmp_init.  Returns the cap
+ * in use or NMP_E_ARG.  The side buffer (31 reals + 1 index per column of the
+ * largest launch on a stream) is allocated stream-ordered at first use. */
+int nmp_set_vege_cap(nmp_engine* eng, int k);
+
 #define NMP_LAUNCH_AUTO 0
 #define NMP_LAUNCH_SMALL 1
 #define NMP_LAUNCH_FULL 2

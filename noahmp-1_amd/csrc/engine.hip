@@ -13,6 +13,7 @@
 #include <cstring>
 #include <mutex>
 #include <new>
+#include <unordered_map>
 #include <vector>
 
 #include "dev_params.h"
@@ -40,9 +41,26 @@ struct nmp_engine {
   // the host entries share hstream and scratch: one at a time per engine
   // (two threads calling them on one engine are serialized here)
   std::mutex host_mu;
+  // Cap and resume of the canopy Newton loop (nmp_set_vege_cap): the cap
+  // (0 = off) and, per stream that launches, the side buffer of the capped
+  // columns -- launches on different streams run concurrently, each needs its
+  // own.  Allocated stream-ordered on first use (hipMallocAsync), grown when a
+  // launch holds more columns, freed by nmp_finalize.
+  int cap_k;
+  struct CapBuf {
+    int32_t* count = nullptr;
+    int32_t* list = nullptr;
+    void* ctx = nullptr;
+    int64_t slots = 0;
+  };
+  std::unordered_map<hipStream_t, CapBuf> cap_bufs;
+  std::mutex cap_mu;
 };
 
 namespace {
+
+// default cap of the canopy Newton loop (nmp_set_vege_cap; 0 = no cap)
+constexpr int kDefaultVegeCap = 0;
 
 bool options_ok(const nmp_options& o) {
   // valid values of each option (core/module_noahmp_global.f90:17-74)
@@ -137,6 +155,33 @@ void fill_args(nmp::KArgs<T>& a, const nmp_engine* e, int64_t ncol, int64_t ld,
   a.cost = cost;
   a.ficeold = static_cast<const T*>(ficeold);
   a.cpw = cols_per_wave(e, ncol);
+  a.cap_k = 0;
+  a.cap_count = a.cap_list = nullptr;
+  a.cap_ctx = nullptr;
+  a.cap_ld = 0;
+}
+
+// The side buffer of stream `s` for a launch of n columns (cap and resume):
+// a counter, the column list and the loop context, kCapFields x slots reals.
+nmp_engine::CapBuf* cap_buffer(nmp_engine* e, hipStream_t s, int64_t n) {
+  std::lock_guard<std::mutex> lk(e->cap_mu);
+  nmp_engine::CapBuf& b = e->cap_bufs[s];
+  if (b.slots >= n && b.count) return &b;
+  if (b.count) {  // stream-ordered: the stream's earlier launches finish first
+    (void)hipFreeAsync(b.count, s);
+    (void)hipFreeAsync(b.list, s);
+    (void)hipFreeAsync(b.ctx, s);
+    b = nmp_engine::CapBuf{};
+  }
+  const int64_t slots = n + n / 8;
+  if (hipMallocAsync((void**)&b.count, 64, s) != hipSuccess ||
+      hipMallocAsync((void**)&b.list, (size_t)slots * sizeof(int32_t), s) != hipSuccess ||
+      hipMallocAsync(&b.ctx, (size_t)slots * nmp::kCapFields * e->precision, s) != hipSuccess) {
+    b = nmp_engine::CapBuf{};
+    return nullptr;
+  }
+  b.slots = slots;
+  return &b;
 }
 
 int launch(nmp_engine* e, int64_t ncol, int64_t ld, const float zsoil[4], float dt,
@@ -150,6 +195,24 @@ int launch(nmp_engine* e, int64_t ncol, int64_t ld, const float zsoil[4], float 
     fill_args(a, e, ncol, ld, zsoil, dt, julian, yearlen, state, isnow, sf, si, fc, diag,
               diag_level, status, order, cost, ficeold);
     const bool small = small_launch(e, ncol);
+    // cap and resume: the production kernels (fp32 "ref", full occupancy, a
+    // compiled option set), plain launches of 64 columns per wave
+    if (e->cap_k > 0 && ncol > 0 && e->math == 0 && !small && e->os != 0 && !order && !cost &&
+        a.cpw == 64) {
+      nmp_engine::CapBuf* b = cap_buffer(e, stream, ncol);
+      if (!b) return NMP_E_DEVICE;
+      a.cap_k = e->cap_k;
+      a.cap_count = b->count;
+      a.cap_list = b->list;
+      a.cap_ctx = static_cast<float*>(b->ctx);
+      a.cap_ld = b->slots;
+      if (hipMemsetAsync(b->count, 0, sizeof(int32_t), stream) != hipSuccess) return NMP_E_DEVICE;
+      err = nmp::launch_sflx<float, true>(e->dparams, a, stream, false, e->os, nmp::kModeCapped);
+      if (err == hipSuccess)
+        err = nmp::launch_sflx<float, true>(e->dparams, a, stream, false, e->os,
+                                            nmp::kModeResume);
+      return err == hipSuccess ? NMP_OK : NMP_E_DEVICE;
+    }
     err = (e->math == 0) ? nmp::launch_sflx<float, true>(e->dparams, a, stream, small, e->os)
                          : nmp::launch_sflx<float, false>(e->dparams, a, stream, small, 0);
   } else {
@@ -261,6 +324,11 @@ int nmp_init(const nmp_params* params, const nmp_options* opts, int device, int 
   e->dparams = d;
   e->scratch = nullptr;
   e->scratch_bytes = 0;
+  // NMP_VEGE_CAP=K: cap and resume of the canopy Newton loop at K iterations
+  // (nmp_set_vege_cap); default kDefaultVegeCap
+  const char* vc = std::getenv("NMP_VEGE_CAP");
+  e->cap_k = vc ? std::atoi(vc) : kDefaultVegeCap;
+  if (e->cap_k < 0 || e->cap_k > 19) e->cap_k = 0;
   if (hipStreamCreateWithFlags(&e->hstream, hipStreamNonBlocking) != hipSuccess) {
     hipFree(d);
     delete e;
@@ -287,6 +355,12 @@ int nmp_option_set(nmp_engine* eng, int request) {
   if (request == 0) eng->os = 0;
   if (request == 1) eng->os = option_set(eng->opts);
   return eng->os;
+}
+
+int nmp_set_vege_cap(nmp_engine* eng, int k) {
+  if (!eng || k < -1 || k > 19 || k == 1) return NMP_E_ARG;
+  if (k >= 0) eng->cap_k = k;
+  return eng->cap_k;
 }
 
 int nmp_set_launch_variant(nmp_engine* eng, int variant) {
@@ -717,6 +791,14 @@ void nmp_finalize(nmp_engine* eng) {
     (void)hipStreamDestroy(eng->hstream);
   }
   if (eng->scratch) hipFree(eng->scratch);
+  if (!eng->cap_bufs.empty()) {
+    (void)hipDeviceSynchronize();  // the launches that used the side buffers
+    for (auto& kv : eng->cap_bufs) {
+      if (kv.second.count) (void)hipFree(kv.second.count);
+      if (kv.second.list) (void)hipFree(kv.second.list);
+      if (kv.second.ctx) (void)hipFree(kv.second.ctx);
+    }
+  }
   if (eng->dparams) hipFree(eng->dparams);
   delete eng;
 }

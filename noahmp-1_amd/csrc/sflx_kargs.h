@@ -47,11 +47,28 @@ struct KArgs {
   // columns stepped per 64-lane wave (8..64, a multiple of 8): below 64 the
   // launch spreads a small column set over more waves (small-N latency hiding)
   int cpw;
+  // Cap and resume of the canopy Newton loop (sflx_kernel.hip, DESIGN.md
+  // "Cap and resume"): in the main launch a lane still iterating after cap_k
+  // iterations appends its column (cap_list) and its loop context (cap_ctx,
+  // [field][slot] with cap_ld slots) at slot atomicAdd(cap_count) and leaves
+  // the step; the resume launch steps the cap_count listed columns on from
+  // that context.  cap_k = 0: no cap.
+  int cap_k;
+  int32_t* cap_count;
+  int32_t* cap_list;
+  T* cap_ctx;
+  int64_t cap_ld;
 };
+
+// launch modes of the step kernel: plain, main launch with the loop capped,
+// resume launch of the capped columns
+enum { kModePlain = 0, kModeCapped = 1, kModeResume = 2 };
+// loop-context fields a capped lane saves (sflx_kernel.hip vege_loop)
+constexpr int kCapFields = 31;
 
 template <class T, bool R>
 hipError_t launch_sflx(const DevParams* dparams, const KArgs<T>& a, hipStream_t stream,
-                       bool small, int os);
+                       bool small, int os, int mode = kModePlain);
 
 // csrc/forcing.hip: synthetic forcing of one step from the climate records
 hipError_t launch_forcing_synth(int precision, int64_t ncol, int64_t ld, const void* clim,

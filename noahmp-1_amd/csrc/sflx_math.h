@@ -31,9 +31,45 @@ namespace nmp {
 template <class T, bool REF>
 struct Mth;
 
+// fp64 exp with a short dependent chain (NMP_F64_EXP_ESTRIN): ocml's own
+// reduction (k = rint(x/ln2), r = x - k ln2 in two parts) and its degree-11
+// Taylor coefficients, but the polynomial evaluated by Estrin's scheme (depth
+// 4 instead of 11 dependent FMAs) and rebuilt with ldexp.  The fp64 path is
+// held to tolerances, not bits (DESIGN.md "fp64"); the result is within an ulp
+// or two of ocml's.  Aimed at config #2, whose one wave per SIMD runs every
+// dependent chain at full latency.
+#ifndef NMP_F64_EXP_ESTRIN
+#define NMP_F64_EXP_ESTRIN 0
+#endif
+__device__ __forceinline__ double exp_estrin(double x) {
+  const double k = __builtin_rint(x * 1.4426950408889634);     // x / ln2
+  double r = __builtin_fma(k, -0.6931471805599453, x);          // ln2, then its tail
+  r = __builtin_fma(k, -2.3190468138462996e-17, r);
+  const double r2 = r * r, r4 = r2 * r2, r8 = r4 * r4;
+  // ocml's coefficients c0..c11 (c0 = c1 = 1), paired by Estrin's scheme
+  const double q0 = __builtin_fma(r, 1.0, 1.0);
+  const double q1 = __builtin_fma(r, 0.16666666666666477, 0.5000000000000012);
+  const double q2 = __builtin_fma(r, 0.008333333333455043, 0.041666666666519754);
+  const double q3 = __builtin_fma(r, 0.00019841269589115522, 0.0013888888945916382);
+  const double q4 = __builtin_fma(r, 2.755751454582531e-06, 2.480149103909504e-05);
+  const double q5 = __builtin_fma(r, 2.502232256764614e-08, 2.7630903490112654e-07);
+  const double s0 = __builtin_fma(r2, q1, q0);
+  const double s1 = __builtin_fma(r2, q3, q2);
+  const double s2 = __builtin_fma(r2, q5, q4);
+  const double p = __builtin_fma(r8, s2, __builtin_fma(r4, s1, s0));
+  const double e = __builtin_ldexp(p, (int)k);
+  // ocml's limits: +inf above 1024, 0 below -1075 (ldexp saturates between);
+  // NaN propagates through r
+  return x > 1024.0 ? __builtin_inf() : (x < -1075.0 ? 0.0 : e);
+}
+
 template <bool REF>
 struct Mth<double, REF> {
+#if NMP_F64_EXP_ESTRIN
+  NMP_MATH_FN double exp(double x) { return exp_estrin(x); }
+#else
   NMP_MATH_FN double exp(double x) { return ::exp(x); }
+#endif
   NMP_MATH_FN double exp2(double x) { return ::exp2(x); }
   NMP_MATH_FN double log(double x) { return ::log(x); }
   NMP_MATH_FN double log10(double x) { return ::log10(x); }
@@ -44,7 +80,7 @@ struct Mth<double, REF> {
   // fp64 path's tolerances, at about half the cost of ocml's double pow (that
   // one carries log x in double-double).  Every base in the kernel is >= 0;
   // 0**y (y > 0) -> exp(-inf) = 0 as pow gives.
-  NMP_MATH_FN double pow(double x, double y) { return ::exp(y * ::log(x)); }
+  NMP_MATH_FN double pow(double x, double y) { return exp(y * ::log(x)); }
 #endif
   // x**0.25 and x**(-0.25): the fp64 path is held to a tolerance, not to bits
   // (DESIGN.md "fp64"), so the fourth root is two square roots (<= 1 ulp from
@@ -131,8 +167,8 @@ __device__ __forceinline__ void pow_pair(T x, T y1, T y2, T& r1, T& r2) {
 #ifndef NMP_F64_OCML_POW
   if constexpr (sizeof(T) == 8) {
     const double lx = ::log(x);
-    r1 = ::exp(y1 * lx);
-    r2 = ::exp(y2 * lx);
+    r1 = Mth<double, R>::exp(y1 * lx);
+    r2 = Mth<double, R>::exp(y2 * lx);
     return;
   }
 #endif

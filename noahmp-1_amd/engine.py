@@ -105,6 +105,14 @@ class Engine:
         _lib.check(min(rc, 0), "nmp_set_launch_variant")
         return {i: k for k, i in LAUNCH_VARIANTS.items()}[rc]
 
+    def vege_cap(self, k: int | None = None) -> int:
+        """nmp_set_vege_cap: cap the canopy Newton loop at k iterations and
+        finish the capped columns in a compacted resume launch (2..19, 0 = off;
+        None only queries).  Returns the cap in use.  Results do not depend on it."""
+        rc = self._lib.nmp_set_vege_cap(self._h, -1 if k is None else int(k))
+        _lib.check(min(rc, 0), "nmp_set_vege_cap")
+        return rc
+
     def set_math(self, mode: int):
         _lib.check(self._lib.nmp_set_math(self._h, int(mode)), "nmp_set_math")
         self.math = int(mode)
@@ -336,11 +344,13 @@ class StreamShards:
     caller reads state or diagnostics."""
 
     def __init__(self, engine: Engine, cs: ColumnState, nshards: int = 2, device=None,
-                 rebin_tile: int = 0, rebin_every: int = 1):
+                 rebin_tile: int = 0, rebin_every: int = 1, launch_cols: int = 0):
         """rebin_tile > 0 turns on column re-binning (nmp_step_binned /
         nmp_rebin): every `rebin_every` steps each range re-sorts its columns
         within tiles of rebin_tile columns by the trip counts the previous step
-        recorded, and the next launches step them in that order."""
+        recorded, and the next launches step them in that order.
+        launch_cols > 0 (launch-size study): each range is stepped as
+        sequential launches of at most launch_cols columns on its stream."""
         n = cs.ncol
         nshards = max(1, min(int(nshards), max(n, 1)))
         self.engine, self.cs = engine, cs
@@ -348,6 +358,8 @@ class StreamShards:
         self.streams = [torch.cuda.Stream(dev) for _ in range(nshards)]
         self.ranges = [(n * i // nshards, n * (i + 1) // nshards) for i in range(nshards)]
         self.rebin_tile, self.rebin_every, self.nstep = int(rebin_tile), max(1, int(rebin_every)), 0
+        self.launch_cols = int(launch_cols)
+        assert not (self.launch_cols and self.rebin_tile), "launch_cols: plain launches only"
         self.order = self.cost = None
         if self.rebin_tile:
             # identity order to start with, relative to each range's first column
@@ -385,9 +397,15 @@ class StreamShards:
                 events[i][0].record(st)
             if self.rebin_tile and self.nstep > 0 and self.nstep % self.rebin_every == 0:
                 self.engine.rebin(self.cost, self.order, self.rebin_tile, stream=st, cols=rng)
-            self.engine.step(self.cs, forcing, zsoil, dt, julian, yearlen, diag, diag_level,
-                             stream=st, cols=None if len(self.streams) == 1 else rng,
-                             order=self.order, cost=self.cost)
+            if self.launch_cols:
+                for lo in range(rng[0], rng[1], self.launch_cols):
+                    self.engine.step(self.cs, forcing, zsoil, dt, julian, yearlen, diag,
+                                     diag_level, stream=st,
+                                     cols=(lo, min(lo + self.launch_cols, rng[1])))
+            else:
+                self.engine.step(self.cs, forcing, zsoil, dt, julian, yearlen, diag, diag_level,
+                                 stream=st, cols=None if len(self.streams) == 1 else rng,
+                                 order=self.order, cost=self.cost)
             if events is not None:
                 events[i][1].record(st)
         self.nstep += 1

@@ -111,6 +111,7 @@ def load(build_if_missing: bool = False):
     lib.nmp_sflx_column.argtypes = [vp, vp]
     lib.nmp_option_set.argtypes = [vp, C.c_int]
     lib.nmp_set_launch_variant.argtypes = [vp, C.c_int]
+    lib.nmp_set_vege_cap.argtypes = [vp, C.c_int]
     lib.nmp_type_size.argtypes = [C.c_int]
     lib.nmp_type_size.restype = C.c_int64
     lib.nmp_frh2o.argtypes = [vp, C.c_int64, vp, vp, vp, vp, vp, vp, vp]
@@ -133,7 +134,7 @@ EXPORTED_SYMBOLS = ["nmp_read_tables", "nmp_init", "nmp_step", "nmp_step_binned"
                     "nmp_run", "nmp_run_out", "nmp_frh2o", "nmp_frh2o_host", "nmp_calhum",
                     "nmp_calhum_host",
                     "nmp_state_from_aos", "nmp_sflx_columns", "nmp_sflx_column",
-                    "nmp_engine_info", "nmp_option_set", "nmp_set_launch_variant", "nmp_type_size", "nmp_set_math", "nmp_set_cols_per_wave", "nmp_finalize", "nmp_strerror",
+                    "nmp_engine_info", "nmp_option_set", "nmp_set_launch_variant", "nmp_set_vege_cap", "nmp_type_size", "nmp_set_math", "nmp_set_cols_per_wave", "nmp_finalize", "nmp_strerror",
                     "nmp_abi_version", "nmp_build_hash"]
 
 

@@ -12,7 +12,15 @@
 !                fraction, as the reference harness passes it).
 ! tests/test_gpu_routines.py compares every step with the reference trajectory.
 !
+! Mode "time" (profiles/, DESIGN.md "The Fortran slot timed"): the fixture's
+! columns replicated to <ncol> columns, <nsteps> timed noahmp_run calls after
+! 2 untimed ones, diagnostics (level 1, the 16 output fluxes) copied back on
+! every <out_every>-th step and level 0 otherwise, arrays page-locked or not
+! (<pinned> 1|0).  Writes one line to <out>: ncol nsteps out_every pinned
+! ms_per_run ms_per_fill column_steps_per_s bytes_up_per_step bytes_down_per_step.
+!
 ! usage: engine_drop_in <run|sflx> <tbl_dir> <in.bin> <out.bin>
+!        engine_drop_in time <tbl_dir> <in.bin> <out.txt> <ncol> <nsteps> <out_every> <pinned>
 !   in.bin : int32 n, nsteps, yearlen, options(12); real zsoil(4), dt;
 !            real julian(nsteps); int32 static_i(n,6), isnow(n);
 !            real static_f(n,6), state(n,56), forcing(n,12,nsteps)
@@ -42,6 +50,10 @@ program engine_drop_in
   call noahmp_set_options(opts(1), opts(2), opts(3), opts(4), opts(5), opts(6), &
                           opts(7), opts(8), opts(9), opts(10), opts(11), opts(12))
   nmp_tbl_dir = tbl
+  if (trim(mode) == 'time') then
+     call time_run()
+     stop
+  end if
   call noahmp_columns(n)
   nmp_static_i = si; nmp_isnow = isn; nmp_static_f = sf; nmp_state = st
   nmp_zsoil = zs; nmp_dt = dt; nmp_yearlen = yl; nmp_diag_level = 2
@@ -67,48 +79,103 @@ program engine_drop_in
 
 contains
 
+  subroutine time_run()   ! mode "time": noahmp_run at a production column count
+    character(len=64) :: arg
+    integer :: ncol, nt, oe, pinned, nf, k, i, j
+    integer(8) :: t0, t1, t2, rate, trun, tfill
+    real, allocatable :: frep(:,:,:)
+    real(8) :: ms_run, ms_fill, up, down
+    call get_command_argument(5, arg); read(arg, *) ncol
+    call get_command_argument(6, arg); read(arg, *) nt
+    call get_command_argument(7, arg); read(arg, *) oe
+    call get_command_argument(8, arg); read(arg, *) pinned
+    nf = min(nsteps, 4)
+    call noahmp_columns(ncol)
+    do i = 1, ncol
+       j = mod(i - 1, n) + 1
+       nmp_static_i(i, :) = si(j, :); nmp_isnow(i) = isn(j)
+       nmp_static_f(i, :) = sf(j, :); nmp_state(i, :) = st(j, :)
+    end do
+    allocate(frep(ncol, 12, nf))
+    do k = 1, nf
+       do i = 1, ncol
+          frep(i, :, k) = frc(mod(i - 1, n) + 1, :, k)
+       end do
+    end do
+    nmp_zsoil = zs; nmp_dt = dt; nmp_yearlen = yl
+    nmp_pinned = pinned /= 0
+    call noahmp_init()
+    trun = 0; tfill = 0
+    call system_clock(count_rate=rate)
+    up = 0; down = 0
+    do s = 1, nt + 2
+       k = mod(s - 1, nf) + 1
+       call system_clock(t0)
+       nmp_forcing = frep(:, :, k)          ! the host's own work: filling this step's forcing
+       nmp_julian = jul(k)
+       nmp_diag_level = merge(1, 0, mod(s, oe) == 0)
+       call system_clock(t1)
+       call noahmp_run()
+       call system_clock(t2)
+       if (s > 2) then
+          tfill = tfill + (t1 - t0); trun = trun + (t2 - t1)
+          up = up + 4d0 * 12 * ncol
+          down = down + 4d0 * ncol * (1 + merge(16, 0, nmp_diag_level == 1))
+       end if
+    end do
+    call noahmp_get_state()
+    ms_run = 1d3 * real(trun, 8) / real(rate, 8) / nt
+    ms_fill = 1d3 * real(tfill, 8) / real(rate, 8) / nt
+    open(newunit=v, file=trim(fout), status='replace')
+    write(v, '(i0, 1x, i0, 1x, i0, 1x, i0, 1x, es14.6, 1x, es14.6, 1x, es14.6, 1x, es14.6, 1x, es14.6)') &
+         ncol, nt, oe, pinned, ms_run, ms_fill, ncol / (ms_run * 1d-3), up / nt, down / nt
+    close(v)
+    call noahmp_finalize()
+  end subroutine
+
   subroutine sflx_one(c, s)   ! column c, step s: the reference's calling sequence
     integer, intent(in) :: c, s
     real :: ficeold(-2:0), stc(-2:4), zsnso(-2:4), snice(-2:0), snliq(-2:0), sw(4), smc(4)
-    real :: zlvl, o(58)
+    real :: zlvl, o(58), stl(56)
     integer :: isnow, iz
-    stc = nmp_state(c, 1:7); zsnso = nmp_state(c, 8:14)
-    snice = nmp_state(c, 15:17); snliq = nmp_state(c, 18:20)
-    sw = nmp_state(c, 21:24); smc = nmp_state(c, 25:28)
+    stl = real(nmp_state(c, :))   ! the reference's default real (nmp_rk may be c_double)
+    stc = stl(1:7); zsnso = stl(8:14)
+    snice = stl(15:17); snliq = stl(18:20)
+    sw = stl(21:24); smc = stl(25:28)
     isnow = nmp_isnow(c)
     ficeold = 0.0
     do iz = isnow + 1, 0
        ficeold(iz) = snice(iz) / (snice(iz) + snliq(iz))
     end do
-    zlvl = nmp_static_f(c, 2)
+    zlvl = real(nmp_static_f(c, 2))
     o = 0.0
-    call noahmp_sflx(c, 1, nmp_static_f(c, 1), yl, jul(s), frc(c, 10, s), &
+    call noahmp_sflx(c, 1, real(nmp_static_f(c, 1)), yl, jul(s), frc(c, 10, s), &
          dt, 1000.0, 20.0, 4, nmp_zsoil, 3, &
-         nmp_static_f(c, 3), nmp_static_f(c, 4), nmp_static_i(c, 3), nmp_static_i(c, 2), &
+         real(nmp_static_f(c, 3)), real(nmp_static_f(c, 4)), nmp_static_i(c, 3), nmp_static_i(c, 2), &
          nmp_static_i(c, 1), nmp_static_i(c, 6), nmp_static_i(c, 5), &
          nmp_static_i(c, 4), &
          0, &
          frc(c, 1, s), frc(c, 2, s), frc(c, 3, s), frc(c, 4, s), frc(c, 5, s), frc(c, 6, s), &
-         0.0, frc(c, 7, s), frc(c, 8, s), frc(c, 9, s), nmp_static_f(c, 5), frc(c, 11, s), &
-         frc(c, 12, s), nmp_static_f(c, 6), ficeold, 1000.0, zlvl, &
-         nmp_state(c, 40), nmp_state(c, 39), &
-         stc, sw, smc, nmp_state(c, 31), nmp_state(c, 32), nmp_state(c, 33), &
-         nmp_state(c, 34), nmp_state(c, 35), nmp_state(c, 29), nmp_state(c, 30), &
-         nmp_state(c, 36), nmp_state(c, 42), &
-         isnow, zsnso, nmp_state(c, 37), nmp_state(c, 38), snice, snliq, &
-         nmp_state(c, 43), nmp_state(c, 44), nmp_state(c, 45), nmp_state(c, 46), &
-         nmp_state(c, 49), nmp_state(c, 50), &
-         nmp_state(c, 51), nmp_state(c, 52), nmp_state(c, 53), nmp_state(c, 54), &
-         nmp_state(c, 47), nmp_state(c, 48), &
-         nmp_state(c, 55), nmp_state(c, 56), nmp_state(c, 41), &
+         0.0, frc(c, 7, s), frc(c, 8, s), frc(c, 9, s), real(nmp_static_f(c, 5)), frc(c, 11, s), &
+         frc(c, 12, s), real(nmp_static_f(c, 6)), ficeold, 1000.0, zlvl, &
+         stl(40), stl(39), &
+         stc, sw, smc, stl(31), stl(32), stl(33), &
+         stl(34), stl(35), stl(29), stl(30), &
+         stl(36), stl(42), &
+         isnow, zsnso, stl(37), stl(38), snice, snliq, &
+         stl(43), stl(44), stl(45), stl(46), &
+         stl(49), stl(50), &
+         stl(51), stl(52), stl(53), stl(54), &
+         stl(47), stl(48), &
+         stl(55), stl(56), stl(41), &
          o(1), o(2), o(3), o(4), o(5), o(6), o(7), o(8), o(9), o(10), o(11), o(12), &
          o(13), o(14), o(15), o(16), o(17), o(18), o(19), o(20), o(21), o(22), o(23), o(24), &
          o(25), o(26), o(27), o(28), o(29), o(30), o(31), o(32), o(33), o(34), o(35), o(36), &
          o(37), o(38), o(39), o(40), o(41), o(42), o(43), o(44), o(45), o(46), o(47), o(48), &
          o(49), o(50), o(51), o(52), o(53), o(54), o(55), o(56), o(57), o(58))
-    nmp_state(c, 1:7) = stc; nmp_state(c, 8:14) = zsnso
-    nmp_state(c, 15:17) = snice; nmp_state(c, 18:20) = snliq
-    nmp_state(c, 21:24) = sw; nmp_state(c, 25:28) = smc
+    stl(1:7) = stc; stl(8:14) = zsnso; stl(15:17) = snice; stl(18:20) = snliq
+    stl(21:24) = sw; stl(25:28) = smc
+    nmp_state(c, :) = stl
     nmp_isnow(c) = isnow
     nmp_diag(c, :) = o
     nmp_status(c) = nmp_sflx_status

@@ -407,6 +407,50 @@ def test_fortran_engine_slot_vs_reference(mode):
 
 
 @pytest.mark.gpu
+def test_fortran_engine_slot_fp64(tmp_path):
+    """INTEGRATION.md's engine slot with its one-line switch to the fp64
+    engine (`nmp_rk = c_double`, tests/lib/engine_drop_in_f64): noahmp_init /
+    noahmp_run over real(c_double) column arrays step the run/case.nml
+    trajectory (96 steps, 32 columns) inside the fp64 path's x10 bar against
+    the reference at every step (golden_io.check_fp64_trajectory_step, as the
+    fp64 engine's own trajectory test)."""
+    import subprocess
+    from golden_io import check_fp64_trajectory_step, load
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    exe = os.path.join(root, "tests", "lib", "engine_drop_in_f64")
+    tbl = os.path.join(root, "oracle", "_ref", "tbl")
+    if not os.path.exists(exe):
+        pytest.fail(f"{exe} missing: run __graft_entry__.build() where /root/reference exists")
+    if not os.path.isdir(tbl):
+        pytest.skip("no TBL files beside the oracle (oracle/_ref/tbl) for nmp_read_tables")
+    g = load("traj_casenml.npz")
+    n, nsteps = g["isnow0"].shape[0], g["forcing"].shape[0]
+    dt = float(g["dt"])
+    jul = np.array([float(g["julian0"]) + s * dt / 86400.0 for s in range(nsteps)], np.float32)
+    fin, fout = str(tmp_path / "in.bin"), str(tmp_path / "out.bin")
+    with open(fin, "wb") as f:
+        for a in (np.array([n, nsteps, int(g["yearlen"])], np.int32),
+                  g["options"].astype(np.int32), g["zsoil"].astype(np.float32),
+                  np.array([dt], np.float32), jul, g["static_i"].astype(np.int32),
+                  g["isnow0"].astype(np.int32), g["static_f"], g["state0"], g["forcing"]):
+            f.write(np.ascontiguousarray(a).tobytes())
+    r = subprocess.run([exe, "run", tbl, fin, fout], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    out = np.fromfile(fout, np.uint8)
+    rec = 8 * n * 56 + 4 * n + 8 * n * 58 + 4 * n
+    assert out.size == nsteps * rec
+    out = out.reshape(nsteps, rec)
+    fr = []
+    for s in range(nsteps):
+        o = out[s]
+        st = o[:8 * 56 * n].view(np.float64).reshape(56, n)
+        isn = o[8 * 56 * n:8 * 56 * n + 4 * n].view(np.int32)
+        dg = o[8 * 56 * n + 4 * n:8 * 114 * n + 4 * n].view(np.float64).reshape(58, n)
+        fr.append(check_fp64_trajectory_step("casenml", s, st, isn, dg, g, s))
+    print(f"fp64 engine slot: mean fraction of columns inside the x10 bar {np.mean(fr):.3f}")
+
+
+@pytest.mark.gpu
 def test_device_short_sqrt_equals_ieee_over_its_range(rt):
     """sqrt_normal32 (csrc/sflx_math.h), used at the range-proven sqrt sites
     (tools/div_proof.py), is IEEE sqrtf bit for bit for every finite x >= 2^-96:

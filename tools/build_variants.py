@@ -151,6 +151,16 @@ VARIANTS = {
     "wt_b64": ("-DNMP_WAVE_TIMING", "-DNMP_BLOCK=64", "-DNMP_PREFETCH=0"),
     "b128_nopf": ("-DNMP_BLOCK=128", "-DNMP_PREFETCH=0"),
     "b64_nopf": ("-DNMP_BLOCK=64", "-DNMP_PREFETCH=0"),
+    # round 5: fp64 exp with an Estrin polynomial (shorter dependent chain,
+    # config #2's one wave per SIMD; sflx_math.h exp_estrin)
+    "f64estrin": {"f64": ["-DNMP_F64_EXP_ESTRIN=1"]},
+    # timing probes (results wrong for the capped lanes): the canopy Newton
+    # loop capped at K iterations, capped lanes leaving the step -- the main
+    # launch of a cap-and-resume split (tools/cap_resume_model.py)
+    "cap8": {"f32": ["-DNMP_VEGE_CAP_PROBE=8"]},
+    "cap10": {"f32": ["-DNMP_VEGE_CAP_PROBE=10"]},
+    "cap12": {"f32": ["-DNMP_VEGE_CAP_PROBE=12"]},
+    "cap14": {"f32": ["-DNMP_VEGE_CAP_PROBE=14"]},
 }
 if __name__ == "__main__":
     names = sys.argv[1:] or list(VARIANTS)

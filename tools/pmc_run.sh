@@ -21,5 +21,9 @@ if [ "${VALU:-1}" = 1 ]; then
   rc=$?; echo "bench SQ rc=$rc"; [ $rc -eq 0 ] || exit $rc
   timeout -k 10 300 rocprofv3 --pmc SQ_INSTS_VALU_ADD_F32 SQ_INSTS_VALU_MUL_F32 SQ_INSTS_VALU_FMA_F32 SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_FMA_F64 SQ_WAVES --kernel-trace --output-format csv -d "$OUT/bench_SQ2" -o run -- python3 "$R/bench.py" --steps 5 --warmup 1 --no-cpu-baseline ${BENCH_ARGS:-} > "$OUT/bench_SQ2.log" 2>&1
   rc=$?; echo "bench SQ2 rc=$rc"; [ $rc -eq 0 ] || exit $rc
+  # lane utilisation of the VALU: thread-cycles of VALU
+  # work over 64 x the waves' VALU cycles, from one pass
+  timeout -k 10 300 rocprofv3 --pmc SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY --kernel-trace --output-format csv -d "$OUT/bench_SQ3" -o run -- python3 "$R/bench.py" --steps 5 --warmup 1 --no-cpu-baseline ${BENCH_ARGS:-} > "$OUT/bench_SQ3.log" 2>&1
+  rc=$?; echo "bench SQ3 rc=$rc"; [ $rc -eq 0 ] || exit $rc
 fi
 find "$OUT" -name "*.csv" | head -20

@@ -106,6 +106,16 @@ def main():
                 res[c] = mean_for(sq, c, KERNEL)[0]  # per dispatch
             except AssertionError:
                 pass
+    sq3 = os.path.join(base, "bench_SQ3")
+    if os.path.isdir(sq3):
+        # VALU lane utilisation (rocprofiler's VALUUtilization expression,
+        # counter_defs.yaml: THREAD_CYCLES_VALU / (ACTIVE_INST_VALU x 64)), both
+        # counters from the same pass and dispatches
+        v = {c: mean_for(sq3, c, KERNEL)[0] for c in
+             ("SQ_THREAD_CYCLES_VALU", "SQ_ACTIVE_INST_VALU", "SQ_INSTS_VALU", "SQ_WAVES",
+              "SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY")}
+        res["lane_pass"] = v
+        res["lane_util"] = v["SQ_THREAD_CYCLES_VALU"] / (64.0 * v["SQ_ACTIVE_INST_VALU"])
     out = os.path.join(ROOT, "profiles", "traffic.json")
     if "--out" in sys.argv:
         out = sys.argv[sys.argv.index("--out") + 1]

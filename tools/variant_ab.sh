@@ -6,6 +6,7 @@ set -u
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 OUT=gpurun_out/${TAG:-vab}; mkdir -p "$OUT"
 CFG5="--kind global --ncol 1036800 --precision 8 --opt-veg 2 --dt 3600 --out-every 1 --forcing device"
+CFG2="--kind casenml --ncol 65536 --precision 8"
 # a variant "lib@VAR=value" runs library lib with that environment variable set
 run() {
   local name=$1 spec=$2; shift 2
@@ -22,7 +23,9 @@ run() {
 for rep in $(seq 1 ${REPS:-2}); do
   for v in default ${VARIANTS:-}; do
     for c in ${CFGS:-3 5}; do
-      if [ "$c" = 5 ]; then run cfg5_${v}_$rep $v $CFG5; else run cfg3_${v}_$rep $v; fi
+      if [ "$c" = 5 ]; then run cfg5_${v}_$rep $v $CFG5
+      elif [ "$c" = 2 ]; then run cfg2_${v}_$rep $v $CFG2
+      else run cfg3_${v}_$rep $v; fi
     done
   done
 done
