@@ -1662,7 +1662,7 @@ DEV void sflx_column(const DevParams& P, const KArgs<T>& A, Col<T>& c, const Sin
           ctx([&](int f, T& v) { cp[f * A.cap_ld] = v; });
           cp[29 * A.cap_ld] = (T)mozsgn;
           cp[30 * A.cap_ld] = (T)liter;
-          A.cap_list[base + rank] = (int32_t)out.col;
+          A.cap_list[base + rank] = (int32_t)(out.st - A.state);  // this column
           return false;
         }
       }

@@ -328,11 +328,14 @@ __device__ __forceinline__ float sqrt_normal32(float x) {
 // reciprocal r = fma(fma(-b, r0, 1), r0, r0) from v_rcp_f32 (shared by every
 // division by the same b), then q = a*r, one fma residual correction and
 // v_div_fixup_f32, which gives zero, infinite and NaN operands their IEEE
-// results.  It equals IEEE a/b bit for bit whenever b is normal with a normal
-// reciprocal, the residual a - b*q is not subnormal (a = 0 or |a| >= 2^-102)
-// and the quotient is normal (tools/fdiv_exhaust.hip: every normal b, every
-// pair of significands, exact scaling by powers of two;
-// profiles/r03/fdiv_exhaust2.txt).
+// results.  It equals IEEE a/b bit for bit whenever |b| is in [2^-126, 2^126]
+// (normal, with a normal reciprocal), the residual a - b*q is not subnormal
+// (a = 0 or |a| >= 2^-102) and |a/b| is in [2^-126, 2^126]
+// (tools/fdiv_exhaust.hip: every normal b, every pair of significands, exact
+// scaling by powers of two; profiles/r03/fdiv_exhaust2.txt; and the region's
+// exponent edges, tests/test_gpu_routines.py).  The region stops short of
+// FLT_MAX on purpose: for quotients within an ulp or two of it the product
+// a*r can round past FLT_MAX and the sequence differs.
 struct DivFast32 {
   __device__ __forceinline__ static float recip(float b) {
     float r = __builtin_amdgcn_rcpf(b);

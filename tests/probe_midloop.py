@@ -86,7 +86,7 @@ def main():
                        "in_loop": {IN_LOOP[b]: int(why[b]) for b in IN_LOOP},
                        "columns_differing": int((~ok).sum())}
                 res["runs"].append(run)
-                ok_all &= bool(ok.all()) and fb > 0 and why[19] > 0 and why[20] > 0
+                ok_all = ok_all and bool(ok.all() and fb > 0 and why[19] > 0 and why[20] > 0)
     res["ok"] = ok_all
     print(json.dumps(res))
     return 0 if ok_all else 1

@@ -118,12 +118,16 @@ __global__ void k_sqrt32_all(unsigned lo, unsigned hi, unsigned long long* bad, 
   if (n) atomicAdd(bad, n);
 }
 
-// DivFast32 at the edges of its exact region (sflx_math.h: b normal with a
-// normal reciprocal, a = 0 or |a| >= 2^-102, quotient normal).  Operands
+// DivFast32 at the edges of its exact region (sflx_math.h and
+// tools/div_proof.py: |b| in [2^-126, 2^126], a = 0 or |a| >= 2^-102, |a/b| in
+// [2^-126, 2^126]).  Operands
 // a = +-(1 + ia/2^23) 2^ea, b = (1 + ib/2^23) 2^eb for ia over [0, 2^23) in
 // steps of sa and ib over [0, 2^23) in steps of sb (offsets oa, ob); pairs
-// whose IEEE quotient is not normal are outside the region and skipped.  Each
-// thread takes one ib value and a chunk of 2^14 consecutive ia steps.
+// whose IEEE quotient lies outside [2^-126, 2^126] are outside the region:
+// not counted in cnt[0]/cnt[1], but their mismatches are counted in cnt[2]
+// (above 2^126 the product a*r can round past FLT_MAX and the short sequence
+// then differs, which is why the proof's region stops at 2^126).  Each thread
+// takes one ib value and a chunk of 2^14 consecutive ia steps.
 // cnt[0] pairs checked, cnt[1] mismatches (short sequence vs IEEE a/b).
 constexpr unsigned kDivChunk = 1u << 14;
 __global__ void k_div32_edge(int ea, int eb, unsigned sa, unsigned oa, unsigned sb, unsigned ob,
@@ -134,14 +138,17 @@ __global__ void k_div32_edge(int ea, int eb, unsigned sa, unsigned oa, unsigned 
   const float b = ldexpf(__uint_as_float(0x3f800000u | (unsigned)ib), eb);
   const nmp::DivFast32 d;
   const nmp::Recip<float> R = d.rec(b);
-  unsigned long long n = 0, nb = 0;
+  unsigned long long n = 0, nb = 0, nout = 0;
   const uint64_t i0 = oa + (k % nchunk) * (uint64_t)kDivChunk * sa;
   for (uint64_t j = 0, ia = i0; j < kDivChunk && ia < (1u << 23); ++j, ia += sa) {
     const float m = __uint_as_float(0x3f800000u | (unsigned)ia);
     const float a = ldexpf((ia & 1) ? -m : m, ea);
     const float w = a / b;
     const float aw = fabsf(w);
-    if (!(aw >= 0x1p-126f && aw <= 3.40282347e38f)) continue;
+    if (!(aw >= 0x1p-126f && aw <= 0x1p126f)) {
+      if (aw <= 3.40282347e38f && __float_as_uint(d.div(a, R)) != __float_as_uint(w)) ++nout;
+      continue;
+    }
     ++n;
     if (__float_as_uint(d.div(a, R)) != __float_as_uint(w)) {
       ++nb;
@@ -150,6 +157,7 @@ __global__ void k_div32_edge(int ea, int eb, unsigned sa, unsigned oa, unsigned 
   }
   if (n) atomicAdd(&cnt[0], n);
   if (nb) atomicAdd(&cnt[1], nb);
+  if (nout) atomicAdd(&cnt[2], nout);
 }
 
 // host helpers: device copies in, one launch, results out (synchronous)
@@ -274,17 +282,17 @@ int rt_sqrt32_all(unsigned lo, unsigned hi, unsigned long long* bad, unsigned* f
   return hipMemcpy(first, df, sizeof(*df), hipMemcpyDeviceToHost) == hipSuccess ? 0 : -4;
 }
 
-// DivFast32 vs IEEE division on one exponent pair (k_div32_edge); cnt2 =
-// {pairs checked, mismatches}
+// DivFast32 vs IEEE division on one exponent pair (k_div32_edge); cnt3 =
+// {pairs in the region, mismatches there, mismatches outside it}
 int rt_div32_edge(int ea, int eb, unsigned sa, unsigned oa, unsigned sb, unsigned ob,
-                  unsigned long long* cnt2, unsigned* first) {
+                  unsigned long long* cnt3, unsigned* first) {
   if (sa == 0 || sb == 0 || oa >= sa || ob >= sb) return -1;
   Dev D;
-  unsigned long long* dc = D.in<unsigned long long>(nullptr, 2);
+  unsigned long long* dc = D.in<unsigned long long>(nullptr, 3);
   unsigned* df = D.in<unsigned>(nullptr, 1);
   if (!dc || !df) return -4;
   const unsigned none = 0xffffffffu;
-  if (hipMemset(dc, 0, 2 * sizeof(*dc)) != hipSuccess ||
+  if (hipMemset(dc, 0, 3 * sizeof(*dc)) != hipSuccess ||
       hipMemcpy(df, &none, sizeof(none), hipMemcpyHostToDevice) != hipSuccess)
     return -4;
   const uint64_t nbv = ((1u << 23) - ob + sb - 1) / sb;               // b values
@@ -294,7 +302,7 @@ int rt_div32_edge(int ea, int eb, unsigned sa, unsigned oa, unsigned sb, unsigne
   hipLaunchKernelGGL(k_div32_edge, dim3((unsigned)((nthr + 255) / 256)), dim3(256), 0, 0, ea, eb,
                      sa, oa, sb, ob, nchunk, dc, df);
   if (hipDeviceSynchronize() != hipSuccess) return -4;
-  if (hipMemcpy(cnt2, dc, 2 * sizeof(*dc), hipMemcpyDeviceToHost) != hipSuccess) return -4;
+  if (hipMemcpy(cnt3, dc, 3 * sizeof(*dc), hipMemcpyDeviceToHost) != hipSuccess) return -4;
   return hipMemcpy(first, df, sizeof(*df), hipMemcpyDeviceToHost) == hipSuccess ? 0 : -4;
 }
 
