@@ -17,10 +17,12 @@
 ! 2 untimed ones, diagnostics (level 1, the 16 output fluxes) copied back on
 ! every <out_every>-th step and level 0 otherwise, arrays page-locked or not
 ! (<pinned> 1|0).  Writes one line to <out>: ncol nsteps out_every pinned
-! ms_per_run ms_per_fill column_steps_per_s bytes_up_per_step bytes_down_per_step.
+! ms_per_run ms_per_fill column_steps_per_s bytes_up_per_step bytes_down_per_step
+! chunks.
 !
 ! usage: engine_drop_in <run|sflx> <tbl_dir> <in.bin> <out.bin>
 !        engine_drop_in time <tbl_dir> <in.bin> <out.txt> <ncol> <nsteps> <out_every> <pinned>
+!                            [<chunks>]   (noahmp_run's pipeline chunks, default the module's)
 !   in.bin : int32 n, nsteps, yearlen, options(12); real zsoil(4), dt;
 !            real julian(nsteps); int32 static_i(n,6), isnow(n);
 !            real static_f(n,6), state(n,56), forcing(n,12,nsteps)
@@ -89,6 +91,9 @@ contains
     call get_command_argument(6, arg); read(arg, *) nt
     call get_command_argument(7, arg); read(arg, *) oe
     call get_command_argument(8, arg); read(arg, *) pinned
+    if (command_argument_count() >= 9) then
+       call get_command_argument(9, arg); read(arg, *) nmp_chunks
+    end if
     nf = min(nsteps, 4)
     call noahmp_columns(ncol)
     do i = 1, ncol
@@ -127,8 +132,9 @@ contains
     ms_run = 1d3 * real(trun, 8) / real(rate, 8) / nt
     ms_fill = 1d3 * real(tfill, 8) / real(rate, 8) / nt
     open(newunit=v, file=trim(fout), status='replace')
-    write(v, '(i0, 1x, i0, 1x, i0, 1x, i0, 1x, es14.6, 1x, es14.6, 1x, es14.6, 1x, es14.6, 1x, es14.6)') &
-         ncol, nt, oe, pinned, ms_run, ms_fill, ncol / (ms_run * 1d-3), up / nt, down / nt
+    write(v, '(i0, 1x, i0, 1x, i0, 1x, i0, 1x, es14.6, 1x, es14.6, 1x, es14.6, 1x, es14.6, 1x, es14.6, &
+         & 1x, i0)') ncol, nt, oe, pinned, ms_run, ms_fill, ncol / (ms_run * 1d-3), up / nt, down / nt, &
+         nmp_chunks
     close(v)
     call noahmp_finalize()
   end subroutine

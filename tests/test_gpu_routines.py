@@ -490,9 +490,10 @@ def test_device_short_sqrt_exhaustive(rt):
 # Exponent pairs (ea, eb) at the edges of DivFast32's exact region: |a| at its
 # smallest exponent (-102) over b near 1 and large; b at the smallest normal
 # exponent (-126, reciprocal near 2^126) and at the largest with a normal
-# reciprocal (125); quotients at the bottom (2^-126) and top (2^127) of the
-# normal range; and the interior reference pair (0, 0).
-DIV_EDGES = [(-102, 0), (-102, -1), (-102, 23), (-102, -126), (0, -126), (1, -126), (-60, -126),
+# reciprocal (125); quotients at the bottom (2^-126) and top (2^126) of the
+# region, and just past the top ((127, -1): outside it, only reported); and
+# the interior reference pair (0, 0).
+DIV_EDGES = [(-102, 0), (-102, -1), (-102, 23), (-102, -126), (0, -126), (-1, -126), (-60, -126),
              (127, 125), (0, 125), (-1, 125), (125, 0), (125, -1), (127, -1), (-126 + 24, 24),
              (0, 0)]
 
