@@ -170,6 +170,9 @@ def parse():
     ap.add_argument("--vege-cap", type=int, default=None,
                     help="cap and resume of the canopy Newton loop at this many iterations "
                          "(nmp_set_vege_cap: 2..19, 0 = off; default: the engine's)")
+    ap.add_argument("--first-range", type=float, default=None,
+                    help="(launch-size study) the first of two stream ranges' share of the "
+                         "columns; default equal ranges")
     ap.add_argument("--launch-cols", type=int, default=0,
                     help="(launch-size study) step each stream's column range as sequential "
                          "launches of at most this many columns (0 = one launch per range)")
@@ -369,7 +372,7 @@ def main():
         clim = torch.as_tensor(cases.climate(cols), device=dev).to(dtype).contiguous()
     gather_dst = 0 if a.gather == "root" else None
     ranges = StreamShards(eng, cs, a.streams, rebin_tile=a.rebin_tile, rebin_every=a.rebin_every,
-                          launch_cols=a.launch_cols)
+                          launch_cols=a.launch_cols, first_frac=a.first_range)
     comm = torch.cuda.Stream(dev) if use_dist else None
     if use_dist:
         # after the range streams exist: RCCL's communicator creates streams of
@@ -457,6 +460,7 @@ def main():
                     tj.get("order", "as-generated") == a.order and \
                     (a.order == "as-generated" or tj.get("order_band", 4.0) == a.order_band) and \
                     tj.get("out_every", 2) == a.out_every and \
+                    tj.get("vege_cap", 0) == eng.vege_cap() and \
                     tj.get("source_hash") == _build.source_hash() \
                     and os.environ.get("NOAHMP_ENGINE_LIB") is None:
                 traffic = tj.get("bytes_per_launch")

@@ -344,19 +344,25 @@ class StreamShards:
     caller reads state or diagnostics."""
 
     def __init__(self, engine: Engine, cs: ColumnState, nshards: int = 2, device=None,
-                 rebin_tile: int = 0, rebin_every: int = 1, launch_cols: int = 0):
+                 rebin_tile: int = 0, rebin_every: int = 1, launch_cols: int = 0,
+                 first_frac: float | None = None):
         """rebin_tile > 0 turns on column re-binning (nmp_step_binned /
         nmp_rebin): every `rebin_every` steps each range re-sorts its columns
         within tiles of rebin_tile columns by the trip counts the previous step
         recorded, and the next launches step them in that order.
         launch_cols > 0 (launch-size study): each range is stepped as
-        sequential launches of at most launch_cols columns on its stream."""
+        sequential launches of at most launch_cols columns on its stream.
+        first_frac (two ranges only): the first range's share of the columns
+        (default: equal ranges)."""
         n = cs.ncol
         nshards = max(1, min(int(nshards), max(n, 1)))
         self.engine, self.cs = engine, cs
         dev = torch.device("cuda", engine.device) if device is None else torch.device(device)
         self.streams = [torch.cuda.Stream(dev) for _ in range(nshards)]
         self.ranges = [(n * i // nshards, n * (i + 1) // nshards) for i in range(nshards)]
+        if first_frac is not None and nshards == 2:
+            cut = min(max(int(round(n * first_frac)) // 256 * 256, 0), n)
+            self.ranges = [(0, cut), (cut, n)]
         self.rebin_tile, self.rebin_every, self.nstep = int(rebin_tile), max(1, int(rebin_every)), 0
         self.launch_cols = int(launch_cols)
         assert not (self.launch_cols and self.rebin_tile), "launch_cols: plain launches only"
