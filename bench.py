@@ -170,6 +170,9 @@ def parse():
     ap.add_argument("--vege-cap", type=int, default=None,
                     help="cap and resume of the canopy Newton loop at this many iterations "
                          "(nmp_set_vege_cap: 2..19, 0 = off; default: the engine's)")
+    ap.add_argument("--stagger", action="store_true",
+                    help="start the stream ranges out of phase (the second range's first "
+                         "step waits for the first range's first launch)")
     ap.add_argument("--first-range", type=float, default=None,
                     help="(launch-size study) the first of two stream ranges' share of the "
                          "columns; default equal ranges")
@@ -372,7 +375,8 @@ def main():
         clim = torch.as_tensor(cases.climate(cols), device=dev).to(dtype).contiguous()
     gather_dst = 0 if a.gather == "root" else None
     ranges = StreamShards(eng, cs, a.streams, rebin_tile=a.rebin_tile, rebin_every=a.rebin_every,
-                          launch_cols=a.launch_cols, first_frac=a.first_range)
+                          launch_cols=a.launch_cols, first_frac=a.first_range,
+                          stagger=a.stagger)
     comm = torch.cuda.Stream(dev) if use_dist else None
     if use_dist:
         # after the range streams exist: RCCL's communicator creates streams of
@@ -407,7 +411,7 @@ def main():
                 clim, jul, yearlen, seed, k, f, first_col=rank * n, stream=st, cols=rng)
         ranges.step(f, cases.CASE_NML_ZSOIL, a.dt, jul, yearlen, d,
                     L.DIAG_OUT_LEVEL if d is not None else L.DIAG_NONE, events=ev, pre=pre)
-        sched.finish(k, producers=ranges.streams)
+        sched.finish(k, producers=ranges.producers)
         return d is not None
 
     for k in range(a.warmup):

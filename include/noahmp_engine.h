@@ -25,7 +25,7 @@
  * nmp_state_from_aos          layout bridge from noahmp_state_t records
  *                                                           core/module_noahmp_type.f90:10-42
  * nmp_finalize, nmp_strerror  (error path of utils `assert`/`stop`, core/module_noahmp_utils.f90:21-53)
- * nmp_set_launch_variant, nmp_set_vege_cap, nmp_type_size, nmp_option_set, nmp_set_math,
+ * nmp_set_launch_variant, nmp_set_vege_cap, nmp_pipe_*, nmp_type_size, nmp_option_set, nmp_set_math,
  *   nmp_set_cols_per_wave     engine tuning / host layout checks (no reference counterpart)
  *
  * Conventions
@@ -428,6 +428,31 @@ int nmp_option_set(nmp_engine* eng, int request);
  * in use or NMP_E_ARG.  The side buffer (31 reals + 1 index per column of the
  * largest launch on a stream) is allocated stream-ordered at first use. */
 int nmp_set_vege_cap(nmp_engine* eng, int k);
+
+/* The cap with the resume off the critical path: a pipeline over one column
+ * set (ncol columns, fp32 engine) that steps on the caller's `stream` and on
+ * a companion stream of its own.  nmp_pipe_step(t) enqueues, on the
+ * companion, the plain step t of the columns capped at step t-1 (finished by
+ * the previous call), on `stream` the main launch of step t (canopy loop
+ * capped at the engine's nmp_set_vege_cap, skipping those columns), and on
+ * the companion the resume launch of step t.  The companion's work runs
+ * beside the next main launch instead of before it.  A column's state,
+ * diagnostics and status are final once nmp_pipe_join has made a stream wait
+ * for both; the companion's work for step t is ordered after everything
+ * enqueued on `stream` before the call (forcing uploads).  Arguments of
+ * nmp_pipe_step as nmp_step's (ncol and stream fixed at creation, the same
+ * `state` every call).  With the cap off, or not applicable (option set 0,
+ * "fast" math, a half-occupancy size), nmp_pipe_step is nmp_step.  Results
+ * are the reference's bits either way (DESIGN.md "Cap and resume"). */
+typedef struct nmp_pipe nmp_pipe;
+int nmp_pipe_create(nmp_engine* eng, int64_t ncol, void* stream, nmp_pipe** out);
+int nmp_pipe_step(nmp_pipe* pipe, int64_t ld, const float zsoil[4], float dt, float julian,
+                  int32_t yearlen, void* state, int32_t* isnow, const void* static_f,
+                  const int32_t* static_i, const void* forcing, void* diag, int diag_level,
+                  int32_t* col_status);
+int nmp_pipe_join(nmp_pipe* pipe, void* stream);
+void* nmp_pipe_stream(nmp_pipe* pipe);
+void nmp_pipe_destroy(nmp_pipe* pipe);
 
 #define NMP_LAUNCH_AUTO 0
 #define NMP_LAUNCH_SMALL 1

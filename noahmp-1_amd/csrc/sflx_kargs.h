@@ -58,11 +58,18 @@ struct KArgs {
   int32_t* cap_list;
   T* cap_ctx;
   int64_t cap_ld;
+  // the deferred pipeline (nmp_pipe_step): the main launch of step
+  // cap_step skips the columns capped at step cap_skip (cap_step_of[c] ==
+  // cap_skip; the companion stream steps them) and records cap_step in
+  // cap_step_of[c] for the columns it caps.  NULL: no skipping.
+  int32_t* cap_step_of;
+  int32_t cap_step, cap_skip;
 };
 
 // launch modes of the step kernel: plain, main launch with the loop capped,
-// resume launch of the capped columns
-enum { kModePlain = 0, kModeCapped = 1, kModeResume = 2 };
+// resume launch of the capped columns, and a plain step of listed columns
+// (the deferred pipeline's step of the previous step's capped columns)
+enum { kModePlain = 0, kModeCapped = 1, kModeResume = 2, kModeListed = 3 };
 // loop-context fields a capped lane saves (sflx_kernel.hip vege_loop)
 constexpr int kCapFields = 31;
 

@@ -1663,6 +1663,7 @@ DEV void sflx_column(const DevParams& P, const KArgs<T>& A, Col<T>& c, const Sin
           cp[29 * A.cap_ld] = (T)mozsgn;
           cp[30 * A.cap_ld] = (T)liter;
           A.cap_list[base + rank] = (int32_t)(out.st - A.state);  // this column
+          if (A.cap_step_of) A.cap_step_of[out.st - A.state] = A.cap_step;
           return false;
         }
       }
@@ -3191,8 +3192,10 @@ void sflx_step_kernel(const DevParams* __restrict__ gparams,
                                                           KArgs<T> a) {
   // the resume launch has the main launch's grid; only the first blocks hold
   // listed columns, the others leave before staging the tables
+  // resume / listed launches: lane gid steps the gid-th listed column
+  constexpr bool kListed = MODE == kModeResume || MODE == kModeListed;
   int64_t nres = 0;
-  if constexpr (MODE == kModeResume) {
+  if constexpr (kListed) {
     nres = *a.cap_count;
     if ((int64_t)blockIdx.x * NMP_BLOCK >= nres) return;
   }
@@ -3226,18 +3229,21 @@ void sflx_step_kernel(const DevParams* __restrict__ gparams,
   const int lane = threadIdx.x & 63;
   if (lane >= a.cpw) return;
   const int64_t gid = (blk * (NMP_BLOCK / 64) + (threadIdx.x >> 6)) * a.cpw + lane;
-  if (gid >= (MODE == kModeResume ? nres : a.ncol)) return;
+  if (gid >= (kListed ? nres : a.ncol)) return;
   // re-binned launch: this lane steps column order[gid] (a permutation of the
   // columns; every column is independent, so results do not depend on it);
-  // resume launch: the gid-th capped column
-  const int64_t c0 = MODE == kModeResume ? (int64_t)a.cap_list[gid]
-                                         : a.order ? (int64_t)a.order[gid] : gid;
+  // resume / listed launch: the gid-th capped column
+  const int64_t c0 = kListed ? (int64_t)a.cap_list[gid] : a.order ? (int64_t)a.order[gid] : gid;
+  // the deferred pipeline's main launch: the previous step's capped columns
+  // are stepped on the companion stream
+  if constexpr (MODE == kModeCapped)
+    if (a.cap_step_of && a.cap_step_of[c0] == a.cap_skip) return;
   const T* st0 = a.state + c0;
   // layer state: through the LDS copy (kPrefetch) or straight from HBM.  The
   // copy is issued first; the column's other fields load while it is in flight
   if constexpr (kPrefetch<T, R>) copy_layers_to_lds(st0, a.ld);
   NMP_LOAD_COLUMN(T, R);
-  sflx_column<T, R, OS, MODE>(sp, a, c, out);
+  sflx_column<T, R, OS, MODE == kModeListed ? kModePlain : MODE>(sp, a, c, out);
   if (c.status != 0) a.status[c0] |= c.status;
 #ifdef NMP_WAVE_TIMING
   {
@@ -3270,14 +3276,20 @@ void launch_os(int os, dim3 grid, dim3 block, hipStream_t stream, const DevParam
       if (os == 1 && mode == kModeCapped)
         hipLaunchKernelGGL((sflx_step_kernel<T, R, SMALL, 1, kModeCapped>), grid, block, 0, stream,
                            dparams, a);
-      else if (os == 1)
+      else if (os == 1 && mode == kModeResume)
         hipLaunchKernelGGL((sflx_step_kernel<T, R, SMALL, 1, kModeResume>), grid, block, 0, stream,
+                           dparams, a);
+      else if (os == 1)
+        hipLaunchKernelGGL((sflx_step_kernel<T, R, SMALL, 1, kModeListed>), grid, block, 0, stream,
                            dparams, a);
       else if (mode == kModeCapped)
         hipLaunchKernelGGL((sflx_step_kernel<T, R, SMALL, 2, kModeCapped>), grid, block, 0, stream,
                            dparams, a);
-      else
+      else if (mode == kModeResume)
         hipLaunchKernelGGL((sflx_step_kernel<T, R, SMALL, 2, kModeResume>), grid, block, 0, stream,
+                           dparams, a);
+      else
+        hipLaunchKernelGGL((sflx_step_kernel<T, R, SMALL, 2, kModeListed>), grid, block, 0, stream,
                            dparams, a);
       return;
     }

@@ -295,11 +295,11 @@ class OfflineDriver:
                              diag if out else None, L.DIAG_OUT_LEVEL if out else L.DIAG_NONE,
                              after=after, pre=pre)
             if self.dev_forcing is None:
-                self.upload.consumed_by(self.ranges.streams)
+                self.upload.consumed_by(self.ranges.producers)
             self.t, self.step_index = t1, self.step_index + 1
             if out:
                 if self.gather is not None:
-                    self.gather.start(b, producers=self.ranges.streams)
+                    self.gather.start(b, producers=self.ranges.producers)
                     d = self.gather.assemble(b)
                     self.n_out += 1
                 else:

@@ -59,7 +59,7 @@ def main():
             jul = 180.0 + k * dt / 86400.0
             ranges.step(torch.as_tensor(F[k], device=dev), cases.CASE_NML_ZSOIL, dt, jul, yl, d,
                         L.DIAG_OUT_LEVEL)
-            sched.finish(k, producers=ranges.streams)
+            sched.finish(k, producers=ranges.producers)
             if gat is None:
                 ranges.join()
                 outs.append(d.clone())

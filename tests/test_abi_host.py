@@ -44,7 +44,7 @@ def _enum_values(text):
 
 
 def test_header_functions_exported(engine_lib):
-    decl = set(re.findall(r"^\s*(?:int|int64_t|void|const char\*)\s+(nmp_\w+)\s*\(", _header(), re.M))
+    decl = set(re.findall(r"^\s*(?:int|int64_t|void\*?|const char\*)\s*(nmp_\w+)\s*\(", _header(), re.M))
     assert decl == set(_lib.EXPORTED_SYMBOLS)
     nm = subprocess.run(["nm", "-D", "--defined-only", _lib.library_path()], capture_output=True,
                         text=True, check=True).stdout

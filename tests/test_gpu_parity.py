@@ -1154,3 +1154,40 @@ def test_vege_cap_stream_ranges_equal_plain(engines):
     assert bit_equal(st1, st0).all() and np.array_equal(isn1, isn0)
     for a, b in zip(out1, out0):
         assert bit_equal(a, b).all()
+
+
+@pytest.mark.parametrize("k", [2, 10])
+def test_vege_cap_pipeline_steps_bit_exact(engines, k):
+    """The deferred cap-and-resume pipeline (nmp_pipe_*, Engine.pipe): the
+    columns capped at step t finish on the companion stream, and take step t+1
+    there too while the caller's stream runs step t+1 of the others.  One
+    pipeline over 65,536 + 77 mixed columns, 8 steps with all 58 outputs
+    every step, the canopy loop capped at k (2: nearly every vegetated lane
+    goes through the companion; 10: the stragglers): after each step's join,
+    state, ISNOW, status and outputs equal the uncapped engine's bit for bit."""
+    from noahmp_amd.engine import ColumnState
+    P = __import__("noahmp_amd.params", fromlist=["Params"]).Params.builtin()
+    opts = tuple(L.CASE_NML_OPTIONS[kk] for kk in L.OPTION_NAMES)
+    n = 65536 + 77
+    cols = cases.make_columns(n, "mixed", P.as_dict(), seed=79, julian=180.0)
+    F = [torch.as_tensor(cases.forcing_step(cols, 180.0 + s / 48.0, 366, s, seed=79), device=DEV)
+         for s in range(8)]
+    ref_eng = engines(opts, variant="full")
+    eng = engines(opts, variant=f"full_cap{k}")
+    a, b = ColumnState.from_host(cols, DEV), ColumnState.from_host(cols, DEV)
+    pipe = eng.pipe(b)
+    for s in range(8):
+        da = torch.zeros((L.NDIAG_FULL, n), device=DEV)
+        db = torch.zeros((L.NDIAG_FULL, n), device=DEV)
+        ref_eng.step(a, F[s], cases.CASE_NML_ZSOIL, 1800.0, 180.0 + s / 48.0, 366, da,
+                     L.DIAG_FULL_LEVEL)
+        pipe.step(F[s], cases.CASE_NML_ZSOIL, 1800.0, 180.0 + s / 48.0, 366, db,
+                  L.DIAG_FULL_LEVEL)
+        pipe.join()
+        torch.cuda.synchronize()
+        ok = bit_equal(b.state.cpu().numpy(), a.state.cpu().numpy()).all(0) & \
+            bit_equal(db.cpu().numpy(), da.cpu().numpy()).all(0) & \
+            (b.isnow.cpu().numpy() == a.isnow.cpu().numpy()) & \
+            (b.status.cpu().numpy() == a.status.cpu().numpy())
+        assert ok.all(), f"cap {k}, step {s}: {(~ok).sum()} of {n} columns differ"
+    pipe.close()
