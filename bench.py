@@ -152,8 +152,11 @@ def parse():
                     help="column order on the GPU (columns are independent: any permutation "
                          "gives bit-identical per-column results); 'lon' groups columns of "
                          "similar solar time into the same wave, like a real lat-lon grid")
-    ap.add_argument("--order-band", type=float, default=4.0,
-                    help="longitude band (degrees) of the coherent column orders")
+    ap.add_argument("--order-band", type=float, default=None,
+                    help="longitude band (degrees) of the coherent column orders; default 4, "
+                         "32 for the conus kind (its 27 types leave few columns per key in a "
+                         "524,288-column shard: +4.6 %%, DESIGN.md \"Launch size and config "
+                         "#4's shard\")")
     ap.add_argument("--rebin-tile", type=int, default=0,
                     help="column re-binning (nmp_rebin): sort columns by the previous step's "
                          "vege_flux trip count within tiles of this many columns (0 = off)")
@@ -184,7 +187,10 @@ def parse():
                          "the ordered set R times: the waves of a small set in a large launch")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic.json"),
                     help="PMC-measured HBM bytes per launch (written by tools/pmc_traffic.py)")
-    return ap.parse_args()
+    a = ap.parse_args()
+    if a.order_band is None:
+        a.order_band = 32.0 if a.kind == "conus" else 4.0
+    return a
 
 
 def _free_port() -> int:

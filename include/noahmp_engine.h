@@ -435,7 +435,9 @@ int nmp_set_vege_cap(nmp_engine* eng, int k);
  * companion, the plain step t of the columns capped at step t-1 (finished by
  * the previous call), on `stream` the main launch of step t (canopy loop
  * capped at the engine's nmp_set_vege_cap, skipping those columns), and on
- * the companion the resume launch of step t.  The companion's work runs
+ * the companion the resume launch of step t (`companion`: a stream the caller
+ * keeps alive for the pipeline's lifetime, or NULL for one of the pipeline's
+ * own).  The companion's work runs
  * beside the next main launch instead of before it.  A column's state,
  * diagnostics and status are final once nmp_pipe_join has made a stream wait
  * for both; the companion's work for step t is ordered after everything
@@ -445,7 +447,8 @@ int nmp_set_vege_cap(nmp_engine* eng, int k);
  * "fast" math, a half-occupancy size), nmp_pipe_step is nmp_step.  Results
  * are the reference's bits either way (DESIGN.md "Cap and resume"). */
 typedef struct nmp_pipe nmp_pipe;
-int nmp_pipe_create(nmp_engine* eng, int64_t ncol, void* stream, nmp_pipe** out);
+int nmp_pipe_create(nmp_engine* eng, int64_t ncol, void* stream, void* companion,
+                    nmp_pipe** out);
 int nmp_pipe_step(nmp_pipe* pipe, int64_t ld, const float zsoil[4], float dt, float julian,
                   int32_t yearlen, void* state, int32_t* isnow, const void* static_f,
                   const int32_t* static_i, const void* forcing, void* diag, int diag_level,

@@ -410,6 +410,7 @@ struct nmp_pipe {
   int64_t ncol;
   hipStream_t s;       // the caller's stream: the main launches
   hipStream_t rs;      // the companion: resume and listed launches
+  bool own_rs;         // created here (destroyed with the pipeline)
   hipEvent_t e_entry, e_main, e_rs, e_listed[2];
   const void* state;   // the column set this pipeline steps (identity check)
   int32_t* count[2];   // per step parity: capped-column count, list, context
@@ -423,7 +424,8 @@ struct nmp_pipe {
 
 extern "C" {
 
-int nmp_pipe_create(nmp_engine* eng, int64_t ncol, void* stream, nmp_pipe** out) {
+int nmp_pipe_create(nmp_engine* eng, int64_t ncol, void* stream, void* companion,
+                    nmp_pipe** out) {
   if (!eng || !out || ncol <= 0 || ncol > INT32_MAX) return NMP_E_ARG;
   if (eng->precision != 4) return NMP_E_ARG;
   if (ensure_device(eng->device) != NMP_OK) return NMP_E_DEVICE;
@@ -436,7 +438,9 @@ int nmp_pipe_create(nmp_engine* eng, int64_t ncol, void* stream, nmp_pipe** out)
   p->cap_k = eng->cap_k;
   p->capped = eng->cap_k > 0 && eng->math == 0 && eng->os != 0 && !small_launch(eng, ncol) &&
               cols_per_wave(eng, ncol) == 64;
-  bool ok = hipStreamCreateWithFlags(&p->rs, hipStreamNonBlocking) == hipSuccess;
+  p->rs = static_cast<hipStream_t>(companion);
+  p->own_rs = !companion;
+  bool ok = companion || hipStreamCreateWithFlags(&p->rs, hipStreamNonBlocking) == hipSuccess;
   for (hipEvent_t* e : {&p->e_entry, &p->e_main, &p->e_rs, &p->e_listed[0], &p->e_listed[1]})
     ok = ok && hipEventCreateWithFlags(e, hipEventDisableTiming) == hipSuccess;
   for (int k = 0; k < 2 && ok; ++k)
@@ -551,7 +555,7 @@ void nmp_pipe_destroy(nmp_pipe* p) {
   if (p->step_of) (void)hipFree(p->step_of);
   for (hipEvent_t ev : {p->e_entry, p->e_main, p->e_rs, p->e_listed[0], p->e_listed[1]})
     if (ev) (void)hipEventDestroy(ev);
-  if (p->rs) (void)hipStreamDestroy(p->rs);
+  if (p->rs && p->own_rs) (void)hipStreamDestroy(p->rs);
   delete p;
 }
 

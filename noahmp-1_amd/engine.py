@@ -351,13 +351,15 @@ class CapPipe:
         self.lo, self.hi = (0, n) if cols is None else (int(cols[0]), int(cols[1]))
         assert 0 <= self.lo < self.hi <= n
         self.stream = stream if stream is not None else torch.cuda.current_stream(engine.device)
+        # the companion is a torch stream, so that its lifetime is torch's: tensors
+        # recorded on it (record_stream) may be freed after the pipeline is gone
+        self.companion = torch.cuda.Stream(self.stream.device)
         h = C.c_void_p()
         _lib.check(engine._lib.nmp_pipe_create(engine._h, self.hi - self.lo,
-                                               C.c_void_p(self.stream.cuda_stream), C.byref(h)),
-                   "nmp_pipe_create")
+                                               C.c_void_p(self.stream.cuda_stream),
+                                               C.c_void_p(self.companion.cuda_stream),
+                                               C.byref(h)), "nmp_pipe_create")
         self._h = h
-        self.companion = torch.cuda.ExternalStream(engine._lib.nmp_pipe_stream(h),
-                                                   device=self.stream.device)
 
     def step(self, forcing: torch.Tensor, zsoil, dt: float, julian: float, yearlen: int,
              diag: torch.Tensor | None = None, diag_level: int = L.DIAG_NONE):

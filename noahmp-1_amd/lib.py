@@ -112,7 +112,7 @@ def load(build_if_missing: bool = False):
     lib.nmp_option_set.argtypes = [vp, C.c_int]
     lib.nmp_set_launch_variant.argtypes = [vp, C.c_int]
     lib.nmp_set_vege_cap.argtypes = [vp, C.c_int]
-    lib.nmp_pipe_create.argtypes = [vp, C.c_int64, vp, C.POINTER(vp)]
+    lib.nmp_pipe_create.argtypes = [vp, C.c_int64, vp, vp, C.POINTER(vp)]
     lib.nmp_pipe_step.argtypes = [vp, C.c_int64, f32p, C.c_float, C.c_float, C.c_int32, vp, vp,
                                   vp, vp, vp, vp, C.c_int, vp]
     lib.nmp_pipe_join.argtypes = [vp, vp]
