@@ -32,7 +32,8 @@
  *  - Plain pointers and sizes only.  All per-column arrays are structure of
  *    arrays, field-major: field f of column c lives at base[f*ld + c]
  *    (ld >= ncol), so one wavefront of 64 lanes reads 64 consecutive columns
- *    of one field per load.
+ *    of one field per load.  ld < 2^29 (536,870,912 columns per call;
+ *    NMP_E_ARG otherwise): the kernel forms a column's byte offset in 32 bits.
  *  - "real" arrays are float when the engine was created with precision 4 and
  *    double with precision 8.  Table values (nmp_params) are always float, as
  *    in the reference (real(r4) module arrays).

@@ -61,6 +61,9 @@ namespace {
 
 // default cap of the canopy Newton loop (nmp_set_vege_cap; 0 = no cap)
 constexpr int kDefaultVegeCap = 0;
+// largest column stride: the kernels form a column's byte offset from a
+// field's base in 32 bits (2^29 columns of 8-byte fp64 values = 4 GiB)
+constexpr int64_t kMaxColumns = int64_t(1) << 29;
 
 bool options_ok(const nmp_options& o) {
   // valid values of each option (core/module_noahmp_global.f90:17-74)
@@ -191,6 +194,9 @@ int launch(nmp_engine* e, int64_t ncol, int64_t ld, const float zsoil[4], float 
            const int32_t* si, const void* fc, void* diag, int diag_level, int32_t* status,
            hipStream_t stream, const int32_t* order = nullptr, uint8_t* cost = nullptr,
            const void* ficeold = nullptr) {
+  // the kernel addresses a column as a 32-bit byte offset from each field's
+  // base (sflx_kernel.hip col_at): column indices below kMaxColumns
+  if (ld >= kMaxColumns) return NMP_E_ARG;
   hipError_t err;
   if (e->precision == 4) {
     nmp::KArgs<float> a;
@@ -246,6 +252,7 @@ int check_common(const nmp_engine* eng, int64_t ncol, int64_t ld, const float zs
                  const int32_t* col_status) {
   if (!zsoil || ld < ncol || !state || !isnow || !static_f || !static_i || !forcing || !col_status)
     return NMP_E_ARG;
+  if (ld >= kMaxColumns) return NMP_E_ARG;
   if (diag_level < NMP_DIAG_NONE || diag_level > NMP_DIAG_FULL) return NMP_E_ARG;
   if (diag_level != NMP_DIAG_NONE && !diag) return NMP_E_ARG;
   if (!(dt > 0.0f) || yearlen <= 0) return NMP_E_ARG;

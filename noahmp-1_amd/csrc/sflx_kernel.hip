@@ -813,50 +813,72 @@ DEV void gst(T* p, T v) {
   else *p = v;
 }
 
+// Column addressing.  Every column array is field-major SoA with the
+// launch's stride `ld`; element (field f, column c) of an array is at
+// base + f*ld + c.  The bases are kernel arguments (SGPRs).  With NMP_OFF32
+// (default) the field's address base + f*ld stays uniform (SGPRs) and the
+// lane adds one 32-bit VGPR, the byte offset c*sizeof(E), the same for every
+// field: the SGPR-base + VGPR-offset form of global loads and stores (column
+// indices below 2^30, which nmp_step's argument checks guarantee).  Without
+// it each access forms a per-lane 64-bit address (two VGPRs), which the
+// register allocator kept live or spilled between a field's load and store.
+#ifndef NMP_OFF32
+#define NMP_OFF32 1
+#endif
+template <class E>
+DEV E* col_at(E* base, int64_t ld, int64_t col, int f) {
+  if constexpr (NMP_OFF32 != 0)
+    return (E*)((char*)(base + f * ld) + (uint32_t)((uint32_t)col * (uint32_t)sizeof(E)));
+  else
+    return base + (f * ld + col);
+}
+
 template <class T>
 struct Sink {
-  T* dg;        // diag + column (NULL when level == NMP_DIAG_NONE)
-  T* st;        // state + column
+  T* dg;        // diag (column 0; NULL when level == NMP_DIAG_NONE)
+  T* st;        // state (column 0)
   int64_t ld;
   int level;
-  const T* sf;        // static_f + column
-  const int32_t* si;  // static_i + column
-  const T* fc;        // forcing + column
-  int32_t* isnow;     // isnow + column
-  uint8_t* cost;      // cost key + column (re-binning), or NULL
-  const T* fice;      // caller FICEOLD + column, or NULL
-  int64_t col;        // the column's index (offset of the pointers above)
+  const T* sf;        // static_f (column 0)
+  const int32_t* si;  // static_i (column 0)
+  const T* fc;        // forcing (column 0)
+  int32_t* isnow;     // isnow (column 0)
+  uint8_t* cost;      // cost key (re-binning), or NULL
+  const T* fice;      // caller FICEOLD, or NULL
+  int64_t col;        // this lane's column
   int64_t cap_slot;   // (kModeResume) the column's slot in the cap side buffer
+  template <class E>
+  DEV E* at(E* base, int f) const { return col_at(base, ld, col, f); }
   // late loads: fields first needed deep in the step are read there, not at
   // kernel entry, so they do not hold registers through the energy phase
-  DEV T ls(int f) const { return gld(st + f * ld); }
-  // state pointer laundered through an empty asm: loads through it are real
+  DEV T ls(int f) const { return gld(at(st, f)); }
+  // state base laundered through an empty asm: loads through it are real
   // re-reads, never forwarded from values loaded earlier in the step
   DEV const T* fresh_state() const {
     const T* p = st;
-    __asm__ volatile("" : "+v"(p));
+    __asm__ volatile("" : "+s"(p));
     return p;
   }
-  DEV T lf(int f) const { return gld(sf + f * ld); }
-  DEV int li(int f) const { return gld(si + f * ld); }
-  DEV T la(int f) const { return gld(fc + f * ld); }
+  DEV T lf(int f) const { return gld(at(sf, f)); }
+  DEV int li(int f) const { return gld(at(si, f)); }
+  DEV T la(int f) const { return gld(at(fc, f)); }
   template <int D>
   DEV void d(T v) const {
     if (level == NMP_DIAG_FULL) {
-      gst(dg + D * ld, v);
+      gst(at(dg, D), v);
     } else if (level == NMP_DIAG_OUT) {
       constexpr int o = out_index(D);
-      if (o >= 0) gst(dg + o * ld, v);
+      if (o >= 0) gst(at(dg, o), v);
     }
   }
   DEV void t2m(T v) const {
-    if (level == NMP_DIAG_OUT) gst(dg + NMP_O_T2M * ld, v);
+    if (level == NMP_DIAG_OUT) gst(at(dg, NMP_O_T2M), v);
   }
-  DEV void s(int f, T v) const { gst(st + f * ld, v); }
-  DEV void isn(int v) const { gst(isnow, (int32_t)v); }
+  DEV void s(int f, T v) const { gst(at(st, f), v); }
+  DEV void isn(int v) const { gst(at(isnow, 0), (int32_t)v); }
   // re-binning key: the vege_flux Newton trip count of this step (0 = no canopy)
   DEV void trips(int n) const {
-    if (cost) *cost = (uint8_t)n;
+    if (cost) *at(cost, 0) = (uint8_t)n;
   }
 };
 
@@ -1662,8 +1684,8 @@ DEV void sflx_column(const DevParams& P, const KArgs<T>& A, Col<T>& c, const Sin
           ctx([&](int f, T& v) { cp[f * A.cap_ld] = v; });
           cp[29 * A.cap_ld] = (T)mozsgn;
           cp[30 * A.cap_ld] = (T)liter;
-          A.cap_list[base + rank] = (int32_t)(out.st - A.state);  // this column
-          if (A.cap_step_of) A.cap_step_of[out.st - A.state] = A.cap_step;
+          A.cap_list[base + rank] = (int32_t)out.col;  // this column
+          if (A.cap_step_of) A.cap_step_of[out.col] = A.cap_step;
           return false;
         }
       }
@@ -1977,7 +1999,7 @@ NMP_UNROLL(NMP_BARE_UNROLL)
       if constexpr (kPfReread<T, R>)
         return lds_pool()[f * NMP_BLOCK + slot];
       else
-        return gld(st + f * out.ld);
+        return gld(col_at(st, out.ld, out.col, f));
     };
 #pragma unroll
     for (int k = 0; k < 7; ++k) {
@@ -2001,7 +2023,7 @@ NMP_UNROLL(NMP_BARE_UNROLL)
   // convention)
   if (out.fice) {
 #pragma unroll
-    for (int j = 0; j < 3; ++j) c.ficeold[j] = out.fice[j * out.ld];
+    for (int j = 0; j < 3; ++j) c.ficeold[j] = *out.at(out.fice, j);
   } else {
 #pragma unroll
     for (int j = 0; j < 3; ++j)
@@ -3137,28 +3159,25 @@ DEV void lds_copy_wait() {
 // spilled VGPRs (fp32 run-time math) and 31 -> 79 (fp64).
 #define NMP_LOAD_COLUMN(T, R)                                                                \
   Col<T> c;                                                                                  \
-  const int64_t ld = a.ld;                                                                   \
-  const T* st = a.state + c0;                                                                \
-  c.tv = gld(st + NMP_S_TV * ld); c.tg = gld(st + NMP_S_TG * ld);                            \
-  c.fwet = gld(st + NMP_S_FWET * ld); c.snowh = gld(st + NMP_S_SNOWH * ld);                  \
-  c.sneqv = gld(st + NMP_S_SNEQV * ld);                                                      \
-  c.lai = gld(st + NMP_S_LAI * ld); c.sai = gld(st + NMP_S_SAI * ld);                        \
+  const Sink<T> out{a.diag, a.state, a.ld, a.diag_level, a.static_f, a.static_i, a.forcing,  \
+                    a.isnow, a.cost, a.ficeold, c0, gid};                                    \
+  c.tv = out.ls(NMP_S_TV); c.tg = out.ls(NMP_S_TG);                                          \
+  c.fwet = out.ls(NMP_S_FWET); c.snowh = out.ls(NMP_S_SNOWH);                                \
+  c.sneqv = out.ls(NMP_S_SNEQV);                                                             \
+  c.lai = out.ls(NMP_S_LAI); c.sai = out.ls(NMP_S_SAI);                                      \
   c.albold = c.tauss = c.qsnow = c.sneqvo = (T)0;                                            \
-  c.isnow = gld(a.isnow + c0);                                                               \
-  const T* sf = a.static_f + c0;                                                             \
-  c.lat = gld(sf + NMP_F_LAT * ld); c.zref = gld(sf + NMP_F_ZLVL * ld);                      \
-  c.shdfac = gld(sf + NMP_F_SHDFAC * ld); c.shdmax = gld(sf + NMP_F_SHDMAX * ld);            \
-  const int32_t* si = a.static_i + c0;                                                       \
-  c.lutyp = gld(si + NMP_I_VEGTYP * ld); c.sltyp = gld(si + NMP_I_SOILTYP * ld);             \
-  c.isc = gld(si + NMP_I_SOILCOLOR * ld);                                                    \
-  c.ist = gld(si + NMP_I_IST * ld); c.ice = gld(si + NMP_I_ICE * ld);                        \
-  const T* fc = a.forcing + c0;                                                              \
-  c.sfctmp = gld(fc + NMP_A_SFCTMP * ld); c.sfcprs = gld(fc + NMP_A_SFCPRS * ld);            \
-  c.psfc = gld(fc + NMP_A_PSFC * ld);                                                        \
-  c.uu = gld(fc + NMP_A_UU * ld); c.vv = gld(fc + NMP_A_VV * ld);                            \
-  c.q2 = gld(fc + NMP_A_Q2 * ld);                                                            \
-  c.soldn = gld(fc + NMP_A_SOLDN * ld); c.lwdn = gld(fc + NMP_A_LWDN * ld);                  \
-  c.cosz = gld(fc + NMP_A_COSZ * ld);                                                        \
+  c.isnow = gld(out.at(a.isnow, 0));                                                         \
+  c.lat = out.lf(NMP_F_LAT); c.zref = out.lf(NMP_F_ZLVL);                                    \
+  c.shdfac = out.lf(NMP_F_SHDFAC); c.shdmax = out.lf(NMP_F_SHDMAX);                          \
+  c.lutyp = out.li(NMP_I_VEGTYP); c.sltyp = out.li(NMP_I_SOILTYP);                           \
+  c.isc = out.li(NMP_I_SOILCOLOR);                                                           \
+  c.ist = out.li(NMP_I_IST); c.ice = out.li(NMP_I_ICE);                                      \
+  c.sfctmp = out.la(NMP_A_SFCTMP); c.sfcprs = out.la(NMP_A_SFCPRS);                          \
+  c.psfc = out.la(NMP_A_PSFC);                                                               \
+  c.uu = out.la(NMP_A_UU); c.vv = out.la(NMP_A_VV);                                          \
+  c.q2 = out.la(NMP_A_Q2);                                                                   \
+  c.soldn = out.la(NMP_A_SOLDN); c.lwdn = out.la(NMP_A_LWDN);                                \
+  c.cosz = out.la(NMP_A_COSZ);                                                               \
   c.status = 0;                                                                              \
   {                                                                                          \
     lds_copy_wait<T, R>();                                                                   \
@@ -3166,7 +3185,7 @@ DEV void lds_copy_wait() {
       if constexpr (kPfEntry<T, R>)                                                          \
         return lds_pool()[f * NMP_BLOCK + threadIdx.x];                                      \
       else                                                                                   \
-        return gld(st + f * ld);                                                             \
+        return out.ls(f);                                                                    \
     };                                                                                       \
     _Pragma("unroll") for (int k = 0; k < 7; ++k) {                                          \
       c.stc[k] = rd(NMP_S_STC + k);                                                          \
@@ -3180,10 +3199,7 @@ DEV void lds_copy_wait() {
       c.sh2o[k] = rd(NMP_S_SH2O + k);                                                        \
       c.smc[k] = rd(NMP_S_SMC + k);                                                          \
     }                                                                                        \
-  }                                                                                          \
-  const Sink<T> out{a.diag ? a.diag + c0 : nullptr, a.state + c0, ld, a.diag_level, sf, si,  \
-                    fc, a.isnow + c0, a.cost ? a.cost + c0 : nullptr,                        \
-                    a.ficeold ? a.ficeold + c0 : nullptr, c0, gid}
+  }
 
 template <class T, bool R, bool SMALL, int OS, int MODE = kModePlain>
 __global__ __launch_bounds__(NMP_BLOCK)
@@ -3244,7 +3260,7 @@ void sflx_step_kernel(const DevParams* __restrict__ gparams,
   if constexpr (kPrefetch<T, R>) copy_layers_to_lds(st0, a.ld);
   NMP_LOAD_COLUMN(T, R);
   sflx_column<T, R, OS, MODE == kModeListed ? kModePlain : MODE>(sp, a, c, out);
-  if (c.status != 0) a.status[c0] |= c.status;
+  if (c.status != 0) *out.at(a.status, 0) |= c.status;
 #ifdef NMP_WAVE_TIMING
   {
     const unsigned long long wt1 = __builtin_amdgcn_s_memrealtime();

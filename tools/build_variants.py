@@ -157,6 +157,8 @@ VARIANTS = {
     # timing probes (results wrong for the capped lanes): the canopy Newton
     # loop capped at K iterations, capped lanes leaving the step -- the main
     # launch of a cap-and-resume split (tools/cap_resume_model.py)
+    # 64-bit per-lane column pointers (the addressing before round 5's 32-bit offsets)
+    "off64": ("-DNMP_OFF32=0",),
     "cap8": {"f32": ["-DNMP_VEGE_CAP_PROBE=8"]},
     "cap10": {"f32": ["-DNMP_VEGE_CAP_PROBE=10"]},
     "cap12": {"f32": ["-DNMP_VEGE_CAP_PROBE=12"]},
