@@ -816,20 +816,29 @@ DEV void gst(T* p, T v) {
 // Column addressing.  Every column array is field-major SoA with the
 // launch's stride `ld`; element (field f, column c) of an array is at
 // base + f*ld + c.  The bases are kernel arguments (SGPRs).  With NMP_OFF32
-// (default) the field's address base + f*ld stays uniform (SGPRs) and the
-// lane adds one 32-bit VGPR, the byte offset c*sizeof(E), the same for every
-// field: the SGPR-base + VGPR-offset form of global loads and stores (column
-// indices below 2^30, which nmp_step's argument checks guarantee).  Without
-// it each access forms a per-lane 64-bit address (two VGPRs), which the
-// register allocator kept live or spilled between a field's load and store.
+// the field's address base + f*ld stays uniform (SGPRs) and the lane adds
+// one 32-bit VGPR, the byte offset c*sizeof(E), the same for every field: the
+// SGPR-base + VGPR-offset form of global loads and stores (column indices
+// below 2^29, which the host's argument checks guarantee).  NMP_OFF32=2
+// (default) also recomputes base + f*ld at every access (a few SALU
+// instructions) rather than letting the compiler keep one live 64-bit base
+// per field, which it spilled to VGPR lanes (94 SGPR spills, 700 v_readlane
+// per step).  Spilled VGPRs of the option-set-1 kernel: 36 with 64-bit
+// per-lane pointers (NMP_OFF32=0), 29 with 1, 9 with 2; config #3 +1.8 % and
+// +0.8 %, config #5 +2.9 % and +3.3 % (profiles/r05/off32_ab.txt).
 #ifndef NMP_OFF32
-#define NMP_OFF32 1
+#define NMP_OFF32 2
 #endif
 template <class E>
 DEV E* col_at(E* base, int64_t ld, int64_t col, int f) {
-  if constexpr (NMP_OFF32 != 0)
+  if constexpr (NMP_OFF32 != 0) {
+#if NMP_OFF32 == 2
+    // an opaque copy of the stride per access: base + f*ld is formed here,
+    // not shared with (and kept live for) the other accesses to field f
+    __asm__ volatile("" : "+s"(ld));
+#endif
     return (E*)((char*)(base + f * ld) + (uint32_t)((uint32_t)col * (uint32_t)sizeof(E)));
-  else
+  } else
     return base + (f * ld + col);
 }
 

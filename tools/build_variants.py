@@ -159,6 +159,12 @@ VARIANTS = {
     # launch of a cap-and-resume split (tools/cap_resume_model.py)
     # 64-bit per-lane column pointers (the addressing before round 5's 32-bit offsets)
     "off64": ("-DNMP_OFF32=0",),
+    "off32": ("-DNMP_OFF32=1",),
+    # the SLP vectorizer back on (the base flags' -fno-slp-vectorize overridden)
+    "slp": ("-fslp-vectorize",),
+    # field bases recomputed per access (no per-field SGPR bases to spill)
+    "off32r": ("-DNMP_OFF32=2",),
+    "off32r_w5": ("-DNMP_OFF32=2", "-DNMP_WAVES_PER_EU=5"),
     "cap8": {"f32": ["-DNMP_VEGE_CAP_PROBE=8"]},
     "cap10": {"f32": ["-DNMP_VEGE_CAP_PROBE=10"]},
     "cap12": {"f32": ["-DNMP_VEGE_CAP_PROBE=12"]},
