@@ -820,19 +820,28 @@ DEV void gst(T* p, T v) {
 // one 32-bit VGPR, the byte offset c*sizeof(E), the same for every field: the
 // SGPR-base + VGPR-offset form of global loads and stores (column indices
 // below 2^29, which the host's argument checks guarantee).  NMP_OFF32=2
-// (default) also recomputes base + f*ld at every access (a few SALU
-// instructions) rather than letting the compiler keep one live 64-bit base
-// per field, which it spilled to VGPR lanes (94 SGPR spills, 700 v_readlane
-// per step).  Spilled VGPRs of the option-set-1 kernel: 36 with 64-bit
-// per-lane pointers (NMP_OFF32=0), 29 with 1, 9 with 2; config #3 +1.8 % and
-// +0.8 %, config #5 +2.9 % and +3.3 % (profiles/r05/off32_ab.txt).
+// also recomputes base + f*ld at every access (a few SALU instructions)
+// rather than letting the compiler keep one live 64-bit base per field,
+// which it spilled to VGPR lanes (94 SGPR spills, 700 v_readlane per step).
+// NMP_OFF32=3 also re-reads the array base itself from the kernel-argument
+// segment at each access (a scalar load) instead of holding the eight bases
+// in SGPRs (892 -> 34 v_readlane).  Spilled VGPRs of the fp32 option-set-1
+// kernel: 36 with 64-bit per-lane pointers (NMP_OFF32=0), 29 with 1, 9 with 2,
+// 6 with 3.  Measured (profiles/r05/off32_ab.txt): 1 over 0 config #3 +1.8 %,
+// config #5 +2.9 %; 2 over 1 +0.8 % and +3.3 %; 3 over 2 config #3 +2.1 %
+// but config #5 -0.9 % and config #2 -6.8 % (fp64).  Default: 3 for the fp32
+// translation unit, 2 for the fp64 one.
 #ifndef NMP_OFF32
+#if defined(NMP_TU) && NMP_TU == 4
+#define NMP_OFF32 3
+#else
 #define NMP_OFF32 2
+#endif
 #endif
 template <class E>
 DEV E* col_at(E* base, int64_t ld, int64_t col, int f) {
   if constexpr (NMP_OFF32 != 0) {
-#if NMP_OFF32 == 2
+#if NMP_OFF32 >= 2
     // an opaque copy of the stride per access: base + f*ld is formed here,
     // not shared with (and kept live for) the other accesses to field f
     __asm__ volatile("" : "+s"(ld));
@@ -841,6 +850,23 @@ DEV E* col_at(E* base, int64_t ld, int64_t col, int f) {
   } else
     return base + (f * ld + col);
 }
+
+#if NMP_OFF32 == 3
+// the array bases re-read from the kernel-argument segment at every access
+// (scalar loads) instead of being held in SGPRs: the step kernel's arguments
+// are (const DevParams*, KArgs<T>), KArgs at byte offset 8 (the code object's
+// .args metadata; every kernel that uses Sink has this signature)
+template <class T>
+DEV const __attribute__((address_space(4))) KArgs<T>* kargs_seg() {
+  const __attribute__((address_space(4))) char* p =
+      (const __attribute__((address_space(4))) char*)__builtin_amdgcn_kernarg_segment_ptr();
+  __asm__ volatile("" : "+s"(p));
+  return (const __attribute__((address_space(4))) KArgs<T>*)(p + 8);
+}
+#define NMP_KBASE(sink_member, karg_member) (kargs_seg<T>()->karg_member)
+#else
+#define NMP_KBASE(sink_member, karg_member) (sink_member)
+#endif
 
 template <class T>
 struct Sink {
@@ -860,7 +886,7 @@ struct Sink {
   DEV E* at(E* base, int f) const { return col_at(base, ld, col, f); }
   // late loads: fields first needed deep in the step are read there, not at
   // kernel entry, so they do not hold registers through the energy phase
-  DEV T ls(int f) const { return gld(at(st, f)); }
+  DEV T ls(int f) const { return gld(at(NMP_KBASE(st, state), f)); }
   // state base laundered through an empty asm: loads through it are real
   // re-reads, never forwarded from values loaded earlier in the step
   DEV const T* fresh_state() const {
@@ -868,23 +894,23 @@ struct Sink {
     __asm__ volatile("" : "+s"(p));
     return p;
   }
-  DEV T lf(int f) const { return gld(at(sf, f)); }
-  DEV int li(int f) const { return gld(at(si, f)); }
-  DEV T la(int f) const { return gld(at(fc, f)); }
+  DEV T lf(int f) const { return gld(at(NMP_KBASE(sf, static_f), f)); }
+  DEV int li(int f) const { return gld(at(NMP_KBASE(si, static_i), f)); }
+  DEV T la(int f) const { return gld(at(NMP_KBASE(fc, forcing), f)); }
   template <int D>
   DEV void d(T v) const {
     if (level == NMP_DIAG_FULL) {
-      gst(at(dg, D), v);
+      gst(at(NMP_KBASE(dg, diag), D), v);
     } else if (level == NMP_DIAG_OUT) {
       constexpr int o = out_index(D);
-      if (o >= 0) gst(at(dg, o), v);
+      if (o >= 0) gst(at(NMP_KBASE(dg, diag), o), v);
     }
   }
   DEV void t2m(T v) const {
-    if (level == NMP_DIAG_OUT) gst(at(dg, NMP_O_T2M), v);
+    if (level == NMP_DIAG_OUT) gst(at(NMP_KBASE(dg, diag), NMP_O_T2M), v);
   }
-  DEV void s(int f, T v) const { gst(at(st, f), v); }
-  DEV void isn(int v) const { gst(at(isnow, 0), (int32_t)v); }
+  DEV void s(int f, T v) const { gst(at(NMP_KBASE(st, state), f), v); }
+  DEV void isn(int v) const { gst(at(NMP_KBASE(isnow, isnow), 0), (int32_t)v); }
   // re-binning key: the vege_flux Newton trip count of this step (0 = no canopy)
   DEV void trips(int n) const {
     if (cost) *at(cost, 0) = (uint8_t)n;

@@ -165,6 +165,12 @@ VARIANTS = {
     # field bases recomputed per access (no per-field SGPR bases to spill)
     "off32r": ("-DNMP_OFF32=2",),
     "off32r_w5": ("-DNMP_OFF32=2", "-DNMP_WAVES_PER_EU=5"),
+    # array bases re-read from the kernel-argument segment per access
+    "off32k": ("-DNMP_OFF32=3",),
+    # base flags re-checked once the spills were gone: MachineLICM and GVN-PRE
+    # back on ("drop": flag pairs removed from build.FLAGS)
+    "licm": {"drop": [("-mllvm", "-disable-machine-licm")]},
+    "pre": {"drop": [("-mllvm", "-enable-pre=false")]},
     "cap8": {"f32": ["-DNMP_VEGE_CAP_PROBE=8"]},
     "cap10": {"f32": ["-DNMP_VEGE_CAP_PROBE=10"]},
     "cap12": {"f32": ["-DNMP_VEGE_CAP_PROBE=12"]},
@@ -173,8 +179,28 @@ VARIANTS = {
 if __name__ == "__main__":
     names = sys.argv[1:] or list(VARIANTS)
     vdir = os.path.join(build.LIB_DIR, "variants")
+    base_flags = list(build.FLAGS)
+
+    def drop(flags, seqs):
+        out, i = [], 0
+        while i < len(flags):
+            for q in seqs:
+                if tuple(flags[i:i + len(q)]) == tuple(q):
+                    i += len(q)
+                    break
+            else:
+                out.append(flags[i])
+                i += 1
+        return out
+
     def one(n):
         v = VARIANTS[n]
+        if isinstance(v, dict) and "drop" in v:  # run alone: build.FLAGS patched
+            build.FLAGS = drop(base_flags, v["drop"])
+            try:
+                return build.build(force=True, verbose=False, out=os.path.join(vdir, f"lib_{n}.so"))
+            finally:
+                build.FLAGS = base_flags
         if isinstance(v, dict):  # per-source flags: {"extra": (...), "f64": [...]}
             sf = dict(build.SOURCE_FLAGS)
             if "f64" in v:
@@ -186,6 +212,9 @@ if __name__ == "__main__":
                                check_asm=not n.startswith("nomcse"))
         return build.build(force=True, verbose=False, out=os.path.join(vdir, f"lib_{n}.so"), extra=v,
                            check_asm=not n.startswith("nomcse"))
+    solo = [n for n in names if isinstance(VARIANTS[n], dict) and "drop" in VARIANTS[n]]
     with ThreadPoolExecutor(2) as ex:
-        list(ex.map(one, names))
+        list(ex.map(one, [n for n in names if n not in solo]))
+    for n in solo:
+        one(n)
     print("built", names)
