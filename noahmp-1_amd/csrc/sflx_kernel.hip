@@ -1036,6 +1036,24 @@ static __device__ unsigned int nmp_fb_reason[32];
 #ifndef NMP_BARE_UNROLL
 #define NMP_BARE_UNROLL sizeof(T) == 4 ? 5 : 1
 #endif
+// Late loads of the flux and water phases (fields first read there), issued
+// where they are first needed (NMP_EARLY_LOADS=0) or a phase earlier, so
+// that their memory latency overlaps the phase before (bit 1: water fields
+// after the flux loops; bit 2: flux fields before btran/rsurf).  Values are
+// the same either way: nothing stores these fields before the loads.
+#ifndef NMP_EARLY_LOADS
+#define NMP_EARLY_LOADS 0
+#endif
+#define NMP_FLUX_LOADS()                                                                     \
+  c.tah = out.ls(NMP_S_TAH); c.eah = out.ls(NMP_S_EAH); c.canliq = out.ls(NMP_S_CANLIQ);     \
+  c.canice = out.ls(NMP_S_CANICE); c.qsfc = out.ls(NMP_S_QSFC); c.cm = out.ls(NMP_S_CM);     \
+  c.ch = out.ls(NMP_S_CH); c.tbot = out.lf(NMP_F_TBOT); c.foln = out.lf(NMP_F_FOLN);         \
+  c.co2air = out.la(NMP_A_CO2AIR); c.o2air = out.la(NMP_A_O2AIR)
+#define NMP_WATER_LOADS()                                                                    \
+  const T prcp_w = out.la(NMP_A_PRCP), uu_w = out.la(NMP_A_UU), vv_w = out.la(NMP_A_VV);     \
+  c.zwt = out.ls(NMP_S_ZWT); c.wa = out.ls(NMP_S_WA); c.wt = out.ls(NMP_S_WT);               \
+  c.wslake = out.ls(NMP_S_WSLAKE);                                                           \
+  c.slptyp = out.li(NMP_I_SLOPETYP)
 #define NMP_STR(x) #x
 #define NMP_UNROLL(n) _Pragma(NMP_STR(unroll n))
 
@@ -1358,6 +1376,10 @@ DEV void sflx_column(const DevParams& P, const KArgs<T>& A, Col<T>& c, const Sin
   else
     emg = (T)P.g.emslake * (L(1.0) - fsno) + L(1.0) * fsno;
   NMP_PHASE(3);
+#if NMP_EARLY_LOADS & 2
+  // the flux phase's fields issued here, their latency under btran/rsurf
+  NMP_FLUX_LOADS();
+#endif
   // soil moisture stress (:1117-1140)
   T btran = L(0.0);
 #pragma unroll
@@ -1413,10 +1435,9 @@ DEV void sflx_column(const DevParams& P, const KArgs<T>& A, Col<T>& c, const Sin
   const T stc_top = dget(c.stc, kt), dz_top = dget(c.dz, kt);
 
   // fields first used by the flux phase
-  c.tah = out.ls(NMP_S_TAH); c.eah = out.ls(NMP_S_EAH); c.canliq = out.ls(NMP_S_CANLIQ);
-  c.canice = out.ls(NMP_S_CANICE); c.qsfc = out.ls(NMP_S_QSFC); c.cm = out.ls(NMP_S_CM);
-  c.ch = out.ls(NMP_S_CH); c.tbot = out.lf(NMP_F_TBOT); c.foln = out.lf(NMP_F_FOLN);
-  c.co2air = out.la(NMP_A_CO2AIR); c.o2air = out.la(NMP_A_O2AIR);
+#if !(NMP_EARLY_LOADS & 2)
+  NMP_FLUX_LOADS();
+#endif
   NMP_PHASE(4);
 // NMP_DOM_MASK (timing probes only, not exact in general): the checks kept
 #ifndef NMP_DOM_MASK
@@ -1940,6 +1961,11 @@ NMP_UNROLL(NMP_BARE_UNROLL)
     chb = ehb;
   }
 
+#if NMP_EARLY_LOADS & 1
+  // the water phase's fields issued here, their latency under aggregation,
+  // thermoprop, tsnosoi and phasechange
+  NMP_WATER_LOADS();
+#endif
   NMP_PHASE(6);
   // tile aggregation (:1246-1282)
   T fira, fsh, fgev, ssoil, fcev, fctr, t2m;
@@ -2329,12 +2355,11 @@ NMP_UNROLL(NMP_BARE_UNROLL)
   NMP_PHASE(9);
   // ===================== water: func.f90:4601-4804 =====================
   // fields first used by the water / carbon phase
-  const T prcp_w = out.la(NMP_A_PRCP), uu_w = out.la(NMP_A_UU), vv_w = out.la(NMP_A_VV);
+#if !(NMP_EARLY_LOADS & 1)
+  NMP_WATER_LOADS();
+#endif
   const T qprecc = L(0.10) * prcp_w;  // atm :517-518
   const T qprecl = L(0.90) * prcp_w;
-  c.zwt = out.ls(NMP_S_ZWT); c.wa = out.ls(NMP_S_WA); c.wt = out.ls(NMP_S_WT);
-  c.wslake = out.ls(NMP_S_WSLAKE);
-  c.slptyp = out.li(NMP_I_SLOPETYP);
   T ecan, etran, runsrf = L(0.0), runsub = L(0.0), qsnbot = L(0.0), ponding1 = L(0.0);
   T ponding2 = L(0.0), fpice = L(0.0), snoflow = L(0.0);
   T qrain, snowhin;

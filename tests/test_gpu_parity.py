@@ -752,6 +752,33 @@ def test_sflx_columns_rejects_what_the_kernel_cannot_honour(engines):
     assert eng.sflx_columns(mk()) is not None
 
 
+def test_column_stride_limit_is_rejected(engines):
+    """The kernels form a column's byte offset from each field's base in 32
+    bits (sflx_kernel.hip col_at), so the host refuses a stride ld >= 2^29
+    (engine.hip kMaxColumns) with NMP_E_ARG before any launch; 2^29 - 1 is
+    only limited by the arrays the caller passes (not exercised: 2^29 columns
+    of state are 120 GB)."""
+    import ctypes as C
+    from noahmp_amd import lib as _lib
+    from noahmp_amd.engine import ColumnState
+    from noahmp_amd.params import Params
+    eng = engines([L.CASE_NML_OPTIONS[k] for k in L.OPTION_NAMES])
+    cols = cases.make_columns(256, "mixed", Params.builtin().as_dict(), seed=3, julian=180.0)
+    cs = ColumnState.from_host(cols, DEV)
+    f = torch.as_tensor(cases.forcing_step(cols, 180.0, 366, 0, seed=3), device=DEV)
+    before = cs.state.clone()
+    zs = (C.c_float * 4)(*[float(z) for z in cases.CASE_NML_ZSOIL])
+    p = lambda t: C.c_void_p(t.data_ptr())  # noqa: E731
+    s = C.c_void_p(torch.cuda.current_stream(DEV).cuda_stream)
+    for ld in (1 << 29, (1 << 31) + 256):
+        rc = eng._lib.nmp_step(eng._h, 256, ld, zs, 1800.0, 180.0, 366, p(cs.state), p(cs.isnow),
+                               p(cs.static_f), p(cs.static_i), p(f), None, L.DIAG_NONE,
+                               p(cs.status), s)
+        assert rc == -1, (ld, rc)  # NMP_E_ARG
+    torch.cuda.synchronize()
+    assert torch.equal(cs.state, before)
+
+
 def test_julian_outside_the_year_is_rejected(engines):
     """The calendar position must be a day of the year, 0 <= julian <=
     yearlen (the reference's phenology indexes its 12-month LAI/SAI tables

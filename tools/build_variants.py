@@ -167,6 +167,10 @@ VARIANTS = {
     "off32r_w5": ("-DNMP_OFF32=2", "-DNMP_WAVES_PER_EU=5"),
     # array bases re-read from the kernel-argument segment per access
     "off32k": ("-DNMP_OFF32=3",),
+    # flux / water phase fields loaded a phase early (NMP_EARLY_LOADS bits)
+    "el1": {"f32": ["-DNMP_EARLY_LOADS=1"]},
+    "el2": {"f32": ["-DNMP_EARLY_LOADS=2"]},
+    "el3": {"f32": ["-DNMP_EARLY_LOADS=3"]},
     # base flags re-checked once the spills were gone: MachineLICM and GVN-PRE
     # back on ("drop": flag pairs removed from build.FLAGS)
     "licm": {"drop": [("-mllvm", "-disable-machine-licm")]},
