@@ -17,8 +17,8 @@ LIB_DIR = os.path.join(PKG, "lib")
 DEFAULT_LIB_PATH = os.path.join(LIB_DIR, "libnoahmp_engine.so")
 # NOAHMP_ENGINE_LIB: a tuning variant (tools/build_variants.py), hash-checked only on request
 LIB_PATH = os.environ.get("NOAHMP_ENGINE_LIB") or DEFAULT_LIB_PATH
-SOURCES = ["engine.hip", "sflx_kernel.hip", "sflx_kernel_f64.hip", "rebin.hip", "forcing.hip",
-           "routines.hip", "tables.cpp"]
+SOURCES = ["engine.hip", "sflx_kernel.hip", "sflx_kernel_f64.hip", "sflx_kernel_f64s.hip",
+           "rebin.hip", "forcing.hip", "routines.hip", "tables.cpp"]
 HEADERS = ["dev_params.h", "sflx_kargs.h", "sflx_math.h", "sflx_routines.h", "glibc_math.h",
            "vege_domain.h"]
 # per-source flags: sflx_kernel.hip is compiled as the fp32 translation unit,
@@ -30,16 +30,21 @@ HEADERS = ["dev_params.h", "sflx_kargs.h", "sflx_math.h", "sflx_routines.h", "gl
 # fp32 translation unit: no SimplifyCFG sinking of instructions common to both
 # arms of a branch (config #3 +0.95 % over 4 interleaved A/B rounds; the fp64
 # kernels measured -1 % with it, profiles/r02/f32only_ab.txt)
-SOURCE_FLAGS = {"sflx_kernel.hip": ["-DNMP_TU=4", "-mllvm", "-simplifycfg-sink-common=false"],
-                "sflx_kernel_f64.hip": []}
+# MachineLICM hoists uniform offsets/constants out of the step and Newton
+# loops and holds them across the whole step: spills 70 -> 42 (single-step
+# kernel) without it; with the round-5 addressing it still costs config #3
+# 2.6 % and config #5 9 %, but gives config #2's fp64 one-wave-per-SIMD
+# kernel +2 % (profiles/r05/retune_ab.txt): on for that translation unit only
+_LICM_OFF = ["-mllvm", "-disable-machine-licm"]
+SOURCE_FLAGS = {src: list(_LICM_OFF) for src in SOURCES}
+SOURCE_FLAGS["sflx_kernel.hip"] = ["-DNMP_TU=4", "-mllvm", "-simplifycfg-sink-common=false",
+                                   *_LICM_OFF]
+SOURCE_FLAGS["sflx_kernel_f64s.hip"] = []
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")
 FLAGS = ["-O3", f"--offload-arch={ARCH}", "-fPIC", "-shared", "-std=c++17",
          "-ffp-contract=off", "-Wno-unused-result", "-Wno-unused-value",
-         # MachineLICM hoists uniform offsets/constants out of the step and
-         # Newton loops and holds them across the whole step: spills 70 -> 42
-         # (single-step kernel) without it
-         "-mllvm", "-disable-machine-licm",
+         # (MachineLICM: off per source, SOURCE_FLAGS)
          # no SLP vectorizer: the packed f32 ops it forms (v_pk_fma/mul/add,
          # same IEEE result per element) need aligned register pairs; without
          # them the fp32 step kernel spills 37 VGPRs instead of 52 (scratch
@@ -102,8 +107,30 @@ def check_device_asm(asm_files, verbose: bool = True):
     if bad:
         raise RuntimeError("device assembly check failed (the object would not hold what the "
                            "compiler selected):\n" + "\n".join(bad))
+    check_kernarg_layout(asm_files)
     if verbose:
         print(f"[noahmp build] device asm re-assembles cleanly ({len(asm_files)} units)", flush=True)
+
+
+def check_kernarg_layout(asm_files):
+    """The fp32 step kernels re-read their array bases from the kernel-argument
+    segment at KArgs' byte offset 8 (sflx_kernel.hip kargs_seg, NMP_OFF32=3).
+    Every sflx_step_kernel's code-object metadata must place its second
+    argument (KArgs, by value) at offset 8; a build where it does not is
+    refused."""
+    import re
+    bad = []
+    for a in asm_files:
+        text = open(a).read()
+        for m in re.finditer(r"\.args:(.*?)\.name:\s+(\S+)", text, re.S):
+            if "sflx_step_kernel" not in m.group(2):
+                continue
+            offs = re.findall(r"\.offset:\s+(\d+)", m.group(1))
+            if len(offs) < 2 or offs[1] != "8":
+                bad.append(f"{m.group(2)}: argument offsets {offs[:2]}")
+    if bad:
+        raise RuntimeError("kernel-argument layout check failed (KArgs not at byte offset 8):\n"
+                           + "\n".join(bad))
 
 
 def build(force: bool = False, verbose: bool = True, out: str | None = None,

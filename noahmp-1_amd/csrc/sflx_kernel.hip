@@ -3378,6 +3378,15 @@ void launch_os(int os, dim3 grid, dim3 block, hipStream_t stream, const DevParam
     hipLaunchKernelGGL((sflx_step_kernel<T, R, SMALL, 0>), grid, block, 0, stream, dparams, a);
 }
 
+// The fp64 half-occupancy (small) kernels live in their own translation unit
+// (NMP_TU 9, sflx_kernel_f64s.hip) with MachineLICM on: config #2's
+// one-wave-per-SIMD kernel runs +2 % with it, the full-occupancy fp64 kernels
+// -9 % (profiles/r05/retune_ab.txt)
+#if defined(NMP_TU) && NMP_TU == 8
+extern template void launch_os<double, false, true>(int, dim3, dim3, hipStream_t,
+                                                    const DevParams*, const KArgs<double>&, int);
+#endif
+
 // launch wrapper (one instantiation per precision / math policy).  os: the
 // compiled option set matching the engine's options (0 = read at run time)
 template <class T, bool R>
@@ -3426,10 +3435,12 @@ extern "C" int nmp_debug_phase_cycles(unsigned long long* out16, int reset) {
 }
 #elif NMP_TU == 4
 int phase_cycles_tu8(unsigned long long* out16, int reset);
+int phase_cycles_tu9(unsigned long long* out16, int reset);
 extern "C" int nmp_debug_phase_cycles(unsigned long long* out16, int reset) {
   for (int i = 0; i < 16; ++i) out16[i] = 0;
-  const int r = phase_cycles_tu4(out16, reset);
-  return r ? r : phase_cycles_tu8(out16, reset);
+  int r = phase_cycles_tu4(out16, reset);
+  if (!r) r = phase_cycles_tu8(out16, reset);
+  return r ? r : phase_cycles_tu9(out16, reset);
 }
 #endif
 #endif
@@ -3476,9 +3487,10 @@ extern "C" long long nmp_debug_wave_records(unsigned long long* out, long long m
 }
 #endif
 
-// Instantiations.  The library compiles this file twice (build.py): NMP_TU 4
-// for the fp32 kernels and NMP_TU 8 (sflx_kernel_f64.hip) for the fp64 ones,
-// each with its own flags; without NMP_TU one object holds both.
+// Instantiations.  The library compiles this file three times (build.py):
+// NMP_TU 4 for the fp32 kernels, NMP_TU 8 (sflx_kernel_f64.hip) for the fp64
+// ones and NMP_TU 9 (sflx_kernel_f64s.hip) for the fp64 small kernels, each
+// with its own flags; without NMP_TU one object holds them all.
 #if !defined(NMP_TU) || NMP_TU == 4
 template hipError_t launch_sflx<float, true>(const DevParams*, const KArgs<float>&, hipStream_t,
                                              bool, int, int);
@@ -3488,6 +3500,10 @@ template hipError_t launch_sflx<float, false>(const DevParams*, const KArgs<floa
 #if !defined(NMP_TU) || NMP_TU == 8
 template hipError_t launch_sflx<double, false>(const DevParams*, const KArgs<double>&, hipStream_t,
                                                bool, int, int);
+#endif
+#if defined(NMP_TU) && NMP_TU == 9
+template void launch_os<double, false, true>(int, dim3, dim3, hipStream_t, const DevParams*,
+                                             const KArgs<double>&, int);
 #endif
 
 }  // namespace nmp

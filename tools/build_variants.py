@@ -168,6 +168,8 @@ VARIANTS = {
     # array bases re-read from the kernel-argument segment per access
     "off32k": ("-DNMP_OFF32=3",),
     # flux / water phase fields loaded a phase early (NMP_EARLY_LOADS bits)
+    # the fp64 small kernels without MachineLICM (the build before the split)
+    "f64s_nolicm": {"f64s": ["-mllvm", "-disable-machine-licm"]},
     "el1": {"f32": ["-DNMP_EARLY_LOADS=1"]},
     "el2": {"f32": ["-DNMP_EARLY_LOADS=2"]},
     "el3": {"f32": ["-DNMP_EARLY_LOADS=3"]},
@@ -201,14 +203,18 @@ if __name__ == "__main__":
         v = VARIANTS[n]
         if isinstance(v, dict) and "drop" in v:  # run alone: build.FLAGS patched
             build.FLAGS = drop(base_flags, v["drop"])
+            sf = {k: drop(f, v["drop"]) for k, f in build.SOURCE_FLAGS.items()}
             try:
-                return build.build(force=True, verbose=False, out=os.path.join(vdir, f"lib_{n}.so"))
+                return build.build(force=True, verbose=False, out=os.path.join(vdir, f"lib_{n}.so"),
+                                   source_flags=sf)
             finally:
                 build.FLAGS = base_flags
         if isinstance(v, dict):  # per-source flags: {"extra": (...), "f64": [...]}
             sf = dict(build.SOURCE_FLAGS)
             if "f64" in v:
-                sf["sflx_kernel_f64.hip"] = list(v["f64"])
+                sf["sflx_kernel_f64.hip"] = list(sf["sflx_kernel_f64.hip"]) + list(v["f64"])
+            if "f64s" in v:  # extra flags for the fp64 small-kernel unit only
+                sf["sflx_kernel_f64s.hip"] = list(sf["sflx_kernel_f64s.hip"]) + list(v["f64s"])
             if "f32" in v:  # extra flags for the fp32 translation unit only
                 sf["sflx_kernel.hip"] = list(sf["sflx_kernel.hip"]) + list(v["f32"])
             return build.build(force=True, verbose=False, out=os.path.join(vdir, f"lib_{n}.so"),
