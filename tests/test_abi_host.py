@@ -255,3 +255,26 @@ def test_stale_library_is_refused(tmp_path, monkeypatch):
     monkeypatch.setattr(lib_mod, "_lib", None)
     with pytest.raises(RuntimeError, match="stale"):
         lib_mod.load()
+
+
+def test_kernarg_layout_check():
+    """The fp32 step kernels read their array bases from the kernel-argument
+    segment at KArgs' byte offset 8 (sflx_kernel.hip kargs_seg); build.py
+    refuses a build whose code-object metadata places it elsewhere."""
+    from noahmp_amd import build
+
+    def meta(off2):
+        return ("  - .args:\n      - .offset: 0\n        .size: 8\n"
+                f"      - .offset: {off2}\n        .size: 240\n        .value_kind: by_value\n"
+                "    .group_segment_fixed_size: 40352\n"
+                "    .name: _ZN3nmp16sflx_step_kernelIfLb1ELb0ELi1ELi0EEEvPKNS_9DevParamsENS_5KArgsIT_EE\n"
+                "  - .args:\n      - .offset: 0\n"
+                "    .name: _ZN3nmp20forcing_synth_kernelIfEEvllPKT_dimllPS1_\n")
+    import tempfile
+    with tempfile.TemporaryDirectory() as td:
+        good, bad = os.path.join(td, "good.s"), os.path.join(td, "bad.s")
+        open(good, "w").write(meta(8))
+        open(bad, "w").write(meta(16))
+        build.check_kernarg_layout([good])
+        with pytest.raises(RuntimeError, match="KArgs not at byte offset 8"):
+            build.check_kernarg_layout([bad])
