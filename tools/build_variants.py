@@ -170,6 +170,10 @@ VARIANTS = {
     # flux / water phase fields loaded a phase early (NMP_EARLY_LOADS bits)
     # the fp64 small kernels without MachineLICM (the build before the split)
     "f64s_nolicm": {"f64s": ["-mllvm", "-disable-machine-licm"]},
+    # machine-scheduler strategies for the fp32 unit
+    "s_ilp": {"f32": ["-mllvm", "-amdgpu-sched-strategy=max-ilp"]},
+    "s_itilp": {"f32": ["-mllvm", "-amdgpu-sched-strategy=iterative-ilp"]},
+    "s_memcl": {"f32": ["-mllvm", "-amdgpu-sched-strategy=max-memory-clause"]},
     "el1": {"f32": ["-DNMP_EARLY_LOADS=1"]},
     "el2": {"f32": ["-DNMP_EARLY_LOADS=2"]},
     "el3": {"f32": ["-DNMP_EARLY_LOADS=3"]},
