@@ -173,6 +173,9 @@ def parse():
     ap.add_argument("--vege-cap", type=int, default=None,
                     help="cap and resume of the canopy Newton loop at this many iterations "
                          "(nmp_set_vege_cap: 2..19, 0 = off; default: the engine's)")
+    ap.add_argument("--cap-same-stream", action="store_true",
+                    help="with --vege-cap: the resume launch on each range's own stream "
+                         "after its capped launch, not the deferred pipeline")
     ap.add_argument("--stagger", action="store_true",
                     help="start the stream ranges out of phase (the second range's first "
                          "step waits for the first range's first launch)")
@@ -382,7 +385,7 @@ def main():
     gather_dst = 0 if a.gather == "root" else None
     ranges = StreamShards(eng, cs, a.streams, rebin_tile=a.rebin_tile, rebin_every=a.rebin_every,
                           launch_cols=a.launch_cols, first_frac=a.first_range,
-                          stagger=a.stagger)
+                          stagger=a.stagger, cap_pipeline=not a.cap_same_stream)
     comm = torch.cuda.Stream(dev) if use_dist else None
     if use_dist:
         # after the range streams exist: RCCL's communicator creates streams of

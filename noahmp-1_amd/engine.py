@@ -402,7 +402,8 @@ class StreamShards:
 
     def __init__(self, engine: Engine, cs: ColumnState, nshards: int = 2, device=None,
                  rebin_tile: int = 0, rebin_every: int = 1, launch_cols: int = 0,
-                 first_frac: float | None = None, stagger: bool = False):
+                 first_frac: float | None = None, stagger: bool = False,
+                 cap_pipeline: bool = True):
         """rebin_tile > 0 turns on column re-binning (nmp_step_binned /
         nmp_rebin): every `rebin_every` steps each range re-sorts its columns
         within tiles of rebin_tile columns by the trip counts the previous step
@@ -412,7 +413,10 @@ class StreamShards:
         first_frac (two ranges only): the first range's share of the columns
         (default: equal ranges).  stagger: the first step of range i > 0 starts
         after range i - 1's first launch, so the ranges run out of phase (their
-        launches' ramp and drain fall on the other range's full waves)."""
+        launches' ramp and drain fall on the other range's full waves).
+        cap_pipeline=False (with the cap on): each range's capped launch and
+        its resume launch run on the range's own stream (nmp_step) instead of
+        the deferred pipeline."""
         n = cs.ncol
         nshards = max(1, min(int(nshards), max(n, 1)))
         self.engine, self.cs = engine, cs
@@ -429,7 +433,7 @@ class StreamShards:
         # one more producer of the range's results
         self.pipes = None
         if engine.precision == 4 and engine.vege_cap() > 0 and not self.rebin_tile \
-                and not self.launch_cols:
+                and not self.launch_cols and cap_pipeline:
             self.pipes = [CapPipe(engine, cs, st, rng if len(self.streams) > 1 else None)
                           for st, rng in zip(self.streams, self.ranges) if rng[1] > rng[0]]
             if len(self.pipes) != len(self.streams):
