@@ -174,6 +174,8 @@ VARIANTS = {
     "s_ilp": {"f32": ["-mllvm", "-amdgpu-sched-strategy=max-ilp"]},
     "s_itilp": {"f32": ["-mllvm", "-amdgpu-sched-strategy=iterative-ilp"]},
     "s_memcl": {"f32": ["-mllvm", "-amdgpu-sched-strategy=max-memory-clause"]},
+    # (timing probe, not exact) the soil-water sub-steps' divisions as a * rcp(b)
+    "soildiv": {"f32": ["-DNMP_SOIL_DIV_PROBE"]},
     "el1": {"f32": ["-DNMP_EARLY_LOADS=1"]},
     "el2": {"f32": ["-DNMP_EARLY_LOADS=2"]},
     "el3": {"f32": ["-DNMP_EARLY_LOADS=3"]},
