@@ -175,6 +175,7 @@ VARIANTS = {
     "s_itilp": {"f32": ["-mllvm", "-amdgpu-sched-strategy=iterative-ilp"]},
     "s_memcl": {"f32": ["-mllvm", "-amdgpu-sched-strategy=max-memory-clause"]},
     # (timing probe, not exact) the soil-water sub-steps' divisions as a * rcp(b)
+    # (needs tools/patches/soil_div_probe.patch applied)
     "soildiv": {"f32": ["-DNMP_SOIL_DIV_PROBE"]},
     "el1": {"f32": ["-DNMP_EARLY_LOADS=1"]},
     "el2": {"f32": ["-DNMP_EARLY_LOADS=2"]},
