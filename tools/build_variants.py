@@ -177,6 +177,8 @@ VARIANTS = {
     # (timing probe, not exact) the soil-water sub-steps' divisions as a * rcp(b)
     # (needs tools/patches/soil_div_probe.patch applied)
     "soildiv": {"f32": ["-DNMP_SOIL_DIV_PROBE"]},
+    # sunlit and shaded stomata solves interleaved (needs tools/patches/stomata_pair.patch)
+    "stpair": {"f32": ["-DNMP_STOMATA_PAIR=1"]},
     "el1": {"f32": ["-DNMP_EARLY_LOADS=1"]},
     "el2": {"f32": ["-DNMP_EARLY_LOADS=2"]},
     "el3": {"f32": ["-DNMP_EARLY_LOADS=3"]},
