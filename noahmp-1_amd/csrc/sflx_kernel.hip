@@ -855,7 +855,9 @@ DEV E* col_at(E* base, int64_t ld, int64_t col, int f) {
 // the array bases re-read from the kernel-argument segment at every access
 // (scalar loads) instead of being held in SGPRs: the step kernel's arguments
 // are (const DevParams*, KArgs<T>), KArgs at byte offset 8 (the code object's
-// .args metadata; every kernel that uses Sink has this signature)
+// .args metadata, which build.py check_kernarg_layout verifies for every
+// sflx_step_kernel of each build; every kernel that uses Sink has this
+// signature)
 template <class T>
 DEV const __attribute__((address_space(4))) KArgs<T>* kargs_seg() {
   const __attribute__((address_space(4))) char* p =
