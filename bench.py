@@ -164,18 +164,20 @@ def parse():
     ap.add_argument("--cpw", type=int, default=0,
                     help="columns per wave (8..64, multiple of 8); 0 = the engine's automatic "
                          "choice (fewer per wave when the column set cannot fill the chip)")
+    ap.add_argument("--emulate-rank", type=int, default=None,
+                    help="(N = 1 only) step the column block rank R of an N-GPU run holds "
+                         "(seed 1000 + R, first global column R * ncol): the shards of a "
+                         "multi-GPU run measured one at a time on one GPU")
+    ap.add_argument("--force-collective", action="store_true",
+                    help="(under a launcher, world 1) issue the output-step collective even "
+                         "though one rank has nothing to exchange: the RCCL code path's own "
+                         "cost on the GPU (its copy kernels), measurable on one GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-steps", type=int, default=32)
     ap.add_argument("--launch-probe", action="store_true",
                     help="launcher check only (CPU tests): every rank joins the process group "
                          "over gloo and contributes its column count, rank 0 prints the line "
                          "with n_gpus and the summed columns; no GPU is touched, no rate")
-    ap.add_argument("--vege-cap", type=int, default=None,
-                    help="cap and resume of the canopy Newton loop at this many iterations "
-                         "(nmp_set_vege_cap: 2..19, 0 = off; default: the engine's)")
-    ap.add_argument("--cap-same-stream", action="store_true",
-                    help="with --vege-cap: the resume launch on each range's own stream "
-                         "after its capped launch, not the deferred pipeline")
     ap.add_argument("--stagger", action="store_true",
                     help="start the stream ranges out of phase (the second range's first "
                          "step waits for the first range's first launch)")
@@ -328,11 +330,16 @@ def main():
     pdict = P.as_dict()
     opt_dict = dict(L.CASE_NML_OPTIONS, opt_veg=a.opt_veg)
     options = L.options_tuple(opt_dict)
-    julian0, yearlen, seed = 180.0, 366, 1000 + rank
+    julian0, yearlen = 180.0, 366
+    if a.emulate_rank is not None and world != 1:
+        print("bench.py: --emulate-rank is a one-GPU measurement", file=sys.stderr, flush=True)
+        sys.exit(2)
+    shard_id = rank if a.emulate_rank is None else a.emulate_rank
+    seed = 1000 + shard_id
     assert a.replicate >= 1 and a.ncol % a.replicate == 0
     ngen = a.ncol // a.replicate
     cols = cases.make_columns(ngen, a.kind, pdict, seed=seed, julian=julian0,
-                              first=rank * a.ncol)
+                              first=shard_id * a.ncol)
     if a.order != "as-generated":
         from noahmp_amd.order import coherent_order
         cols = cols.take(coherent_order(cols.lon, cols.static_i, cols.isnow, a.order,
@@ -366,8 +373,6 @@ def main():
     dtype = torch.float32 if a.precision == 4 else torch.float64
     eng = Engine(P, opt_dict, device=local, precision=a.precision, math=a.math)
     eng.set_cols_per_wave(a.cpw)
-    if a.vege_cap is not None:
-        eng.vege_cap(a.vege_cap)
     from noahmp_amd import lib as _nlib
     build_hash = _nlib.load().nmp_build_hash().decode()  # lib.load refuses a stale library
     cs = ColumnState.from_host(cols, dev, dtype)
@@ -385,7 +390,7 @@ def main():
     gather_dst = 0 if a.gather == "root" else None
     ranges = StreamShards(eng, cs, a.streams, rebin_tile=a.rebin_tile, rebin_every=a.rebin_every,
                           launch_cols=a.launch_cols, first_frac=a.first_range,
-                          stagger=a.stagger, cap_pipeline=not a.cap_same_stream)
+                          stagger=a.stagger)
     comm = torch.cuda.Stream(dev) if use_dist else None
     if use_dist:
         # after the range streams exist: RCCL's communicator creates streams of
@@ -397,7 +402,8 @@ def main():
             dist.init_process_group(backend)
         # double-buffered output-step gather; a receiving rank's engine writes
         # straight into its own slot of the gather buffer (no local copy)
-        gat = shard.DiagGather(L.NDIAG_OUT, world * n, dtype, dev, dst=gather_dst, comm=comm)
+        gat = shard.DiagGather(L.NDIAG_OUT, world * n, dtype, dev, dst=gather_dst, comm=comm,
+                               force_collective=a.force_collective)
         sched = shard.OutputSchedule(a.out_every, gat, streams=ranges.streams)
     else:
         gat = None
@@ -417,7 +423,7 @@ def main():
         else:
             f = F[k % 2]
             pre = lambda st, rng: eng.forcing_synth(  # noqa: E731
-                clim, jul, yearlen, seed, k, f, first_col=rank * n, stream=st, cols=rng)
+                clim, jul, yearlen, seed, k, f, first_col=shard_id * n, stream=st, cols=rng)
         ranges.step(f, cases.CASE_NML_ZSOIL, a.dt, jul, yearlen, d,
                     L.DIAG_OUT_LEVEL if d is not None else L.DIAG_NONE, events=ev, pre=pre)
         sched.finish(k, producers=ranges.producers)
@@ -473,7 +479,7 @@ def main():
                     tj.get("order", "as-generated") == a.order and \
                     (a.order == "as-generated" or tj.get("order_band", 4.0) == a.order_band) and \
                     tj.get("out_every", 2) == a.out_every and \
-                    tj.get("vege_cap", 0) == eng.vege_cap() and \
+                    tj.get("vege_cap", 0) == 0 and \
                     tj.get("source_hash") == _build.source_hash() \
                     and os.environ.get("NOAHMP_ENGINE_LIB") is None:
                 traffic = tj.get("bytes_per_launch")
@@ -499,10 +505,11 @@ def main():
                        "ncol_total": world * n, "dt_s": a.dt, "out_every": a.out_every,
                        "math": a.math, "column_order": a.order, "forcing": a.forcing,
                        "streams": len(ranges.ranges), "cols_per_wave": a.cpw or "auto",
-                       "vege_cap": eng.vege_cap(),
                        "rebin": {"tile": a.rebin_tile, "every": a.rebin_every}
                        if a.rebin_tile else None,
                        "parallelism": f"column-shard x{world}",
+                       "emulated_rank": a.emulate_rank,
+                       "force_collective": a.force_collective or None,
                        "gather": a.gather if use_dist else None,
                        "backend": backend if use_dist else None},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -13,7 +13,6 @@
 #include <cstring>
 #include <mutex>
 #include <new>
-#include <unordered_map>
 #include <vector>
 
 #include "dev_params.h"
@@ -41,26 +40,10 @@ struct nmp_engine {
   // the host entries share hstream and scratch: one at a time per engine
   // (two threads calling them on one engine are serialized here)
   std::mutex host_mu;
-  // Cap and resume of the canopy Newton loop (nmp_set_vege_cap): the cap
-  // (0 = off) and, per stream that launches, the side buffer of the capped
-  // columns -- launches on different streams run concurrently, each needs its
-  // own.  Allocated stream-ordered on first use (hipMallocAsync), grown when a
-  // launch holds more columns, freed by nmp_finalize.
-  int cap_k;
-  struct CapBuf {
-    int32_t* count = nullptr;
-    int32_t* list = nullptr;
-    void* ctx = nullptr;
-    int64_t slots = 0;
-  };
-  std::unordered_map<hipStream_t, CapBuf> cap_bufs;
-  std::mutex cap_mu;
 };
 
 namespace {
 
-// default cap of the canopy Newton loop (nmp_set_vege_cap; 0 = no cap)
-constexpr int kDefaultVegeCap = 0;
 // largest column stride: the kernels form a column's byte offset from a
 // field's base in 32 bits (2^29 columns of 8-byte fp64 values = 4 GiB)
 constexpr int64_t kMaxColumns = int64_t(1) << 29;
@@ -158,35 +141,6 @@ void fill_args(nmp::KArgs<T>& a, const nmp_engine* e, int64_t ncol, int64_t ld,
   a.cost = cost;
   a.ficeold = static_cast<const T*>(ficeold);
   a.cpw = cols_per_wave(e, ncol);
-  a.cap_k = 0;
-  a.cap_count = a.cap_list = nullptr;
-  a.cap_ctx = nullptr;
-  a.cap_ld = 0;
-  a.cap_step_of = nullptr;
-  a.cap_step = a.cap_skip = 0;
-}
-
-// The side buffer of stream `s` for a launch of n columns (cap and resume):
-// a counter, the column list and the loop context, kCapFields x slots reals.
-nmp_engine::CapBuf* cap_buffer(nmp_engine* e, hipStream_t s, int64_t n) {
-  std::lock_guard<std::mutex> lk(e->cap_mu);
-  nmp_engine::CapBuf& b = e->cap_bufs[s];
-  if (b.slots >= n && b.count) return &b;
-  if (b.count) {  // stream-ordered: the stream's earlier launches finish first
-    (void)hipFreeAsync(b.count, s);
-    (void)hipFreeAsync(b.list, s);
-    (void)hipFreeAsync(b.ctx, s);
-    b = nmp_engine::CapBuf{};
-  }
-  const int64_t slots = n + n / 8;
-  if (hipMallocAsync((void**)&b.count, 64, s) != hipSuccess ||
-      hipMallocAsync((void**)&b.list, (size_t)slots * sizeof(int32_t), s) != hipSuccess ||
-      hipMallocAsync(&b.ctx, (size_t)slots * nmp::kCapFields * e->precision, s) != hipSuccess) {
-    b = nmp_engine::CapBuf{};
-    return nullptr;
-  }
-  b.slots = slots;
-  return &b;
 }
 
 int launch(nmp_engine* e, int64_t ncol, int64_t ld, const float zsoil[4], float dt,
@@ -203,24 +157,6 @@ int launch(nmp_engine* e, int64_t ncol, int64_t ld, const float zsoil[4], float 
     fill_args(a, e, ncol, ld, zsoil, dt, julian, yearlen, state, isnow, sf, si, fc, diag,
               diag_level, status, order, cost, ficeold);
     const bool small = small_launch(e, ncol);
-    // cap and resume: the production kernels (fp32 "ref", full occupancy, a
-    // compiled option set), plain launches of 64 columns per wave
-    if (e->cap_k > 0 && ncol > 0 && e->math == 0 && !small && e->os != 0 && !order && !cost &&
-        a.cpw == 64) {
-      nmp_engine::CapBuf* b = cap_buffer(e, stream, ncol);
-      if (!b) return NMP_E_DEVICE;
-      a.cap_k = e->cap_k;
-      a.cap_count = b->count;
-      a.cap_list = b->list;
-      a.cap_ctx = static_cast<float*>(b->ctx);
-      a.cap_ld = b->slots;
-      if (hipMemsetAsync(b->count, 0, sizeof(int32_t), stream) != hipSuccess) return NMP_E_DEVICE;
-      err = nmp::launch_sflx<float, true>(e->dparams, a, stream, false, e->os, nmp::kModeCapped);
-      if (err == hipSuccess)
-        err = nmp::launch_sflx<float, true>(e->dparams, a, stream, false, e->os,
-                                            nmp::kModeResume);
-      return err == hipSuccess ? NMP_OK : NMP_E_DEVICE;
-    }
     err = (e->math == 0) ? nmp::launch_sflx<float, true>(e->dparams, a, stream, small, e->os)
                          : nmp::launch_sflx<float, false>(e->dparams, a, stream, small, 0);
   } else {
@@ -333,11 +269,6 @@ int nmp_init(const nmp_params* params, const nmp_options* opts, int device, int 
   e->dparams = d;
   e->scratch = nullptr;
   e->scratch_bytes = 0;
-  // NMP_VEGE_CAP=K: cap and resume of the canopy Newton loop at K iterations
-  // (nmp_set_vege_cap); default kDefaultVegeCap
-  const char* vc = std::getenv("NMP_VEGE_CAP");
-  e->cap_k = vc ? std::atoi(vc) : kDefaultVegeCap;
-  if (e->cap_k < 0 || e->cap_k > 19) e->cap_k = 0;
   if (hipStreamCreateWithFlags(&e->hstream, hipStreamNonBlocking) != hipSuccess) {
     hipFree(d);
     delete e;
@@ -364,12 +295,6 @@ int nmp_option_set(nmp_engine* eng, int request) {
   if (request == 0) eng->os = 0;
   if (request == 1) eng->os = option_set(eng->opts);
   return eng->os;
-}
-
-int nmp_set_vege_cap(nmp_engine* eng, int k) {
-  if (!eng || k < -1 || k > 19 || k == 1) return NMP_E_ARG;
-  if (k >= 0) eng->cap_k = k;
-  return eng->cap_k;
 }
 
 int nmp_set_launch_variant(nmp_engine* eng, int variant) {
@@ -407,163 +332,6 @@ int nmp_step(nmp_engine* eng, int64_t ncol, int64_t ld, const float zsoil[4], fl
   if (rc != NMP_OK) return rc;
   return launch(eng, ncol, ld, zsoil, dt, julian, yearlen, state, isnow, static_f, static_i,
                 forcing, diag, diag_level, col_status, static_cast<hipStream_t>(stream));
-}
-
-// ---- the deferred cap-and-resume pipeline (nmp_pipe_*) ------------------
-}  // extern "C"
-
-struct nmp_pipe {
-  nmp_engine* eng;
-  int64_t ncol;
-  hipStream_t s;       // the caller's stream: the main launches
-  hipStream_t rs;      // the companion: resume and listed launches
-  bool own_rs;         // created here (destroyed with the pipeline)
-  hipEvent_t e_entry, e_main, e_rs, e_listed[2];
-  const void* state;   // the column set this pipeline steps (identity check)
-  int32_t* count[2];   // per step parity: capped-column count, list, context
-  int32_t* list[2];
-  float* ctx[2];
-  int32_t* step_of;    // per column: the step it was last capped at
-  int64_t t;           // steps issued
-  bool capped;         // the cap applies (fixed at creation)
-  int cap_k;
-};
-
-extern "C" {
-
-int nmp_pipe_create(nmp_engine* eng, int64_t ncol, void* stream, void* companion,
-                    nmp_pipe** out) {
-  if (!eng || !out || ncol <= 0 || ncol > INT32_MAX) return NMP_E_ARG;
-  if (eng->precision != 4) return NMP_E_ARG;
-  if (ensure_device(eng->device) != NMP_OK) return NMP_E_DEVICE;
-  nmp_pipe* p = new (std::nothrow) nmp_pipe{};
-  if (!p) return NMP_E_ARG;
-  p->eng = eng;
-  p->ncol = ncol;
-  p->s = static_cast<hipStream_t>(stream);
-  // the cap applies to the production kernels only (as in launch())
-  p->cap_k = eng->cap_k;
-  p->capped = eng->cap_k > 0 && eng->math == 0 && eng->os != 0 && !small_launch(eng, ncol) &&
-              cols_per_wave(eng, ncol) == 64;
-  p->rs = static_cast<hipStream_t>(companion);
-  p->own_rs = !companion;
-  bool ok = companion || hipStreamCreateWithFlags(&p->rs, hipStreamNonBlocking) == hipSuccess;
-  for (hipEvent_t* e : {&p->e_entry, &p->e_main, &p->e_rs, &p->e_listed[0], &p->e_listed[1]})
-    ok = ok && hipEventCreateWithFlags(e, hipEventDisableTiming) == hipSuccess;
-  for (int k = 0; k < 2 && ok; ++k)
-    ok = hipMalloc((void**)&p->count[k], 64) == hipSuccess &&
-         hipMalloc((void**)&p->list[k], (size_t)ncol * sizeof(int32_t)) == hipSuccess &&
-         hipMalloc((void**)&p->ctx[k], (size_t)ncol * nmp::kCapFields * sizeof(float)) == hipSuccess;
-  ok = ok && hipMalloc((void**)&p->step_of, (size_t)ncol * sizeof(int32_t)) == hipSuccess &&
-       // -16843010: no step's number
-       hipMemsetAsync(p->step_of, 0xFE, (size_t)ncol * sizeof(int32_t), p->s) == hipSuccess &&
-       hipEventRecord(p->e_listed[0], p->s) == hipSuccess &&
-       hipEventRecord(p->e_listed[1], p->s) == hipSuccess;
-  if (!ok) {
-    nmp_pipe_destroy(p);
-    return NMP_E_DEVICE;
-  }
-  *out = p;
-  return NMP_OK;
-}
-
-// One step of the pipeline's column set (step t = the t-th call), enqueued:
-//   companion: (t >= 1) the plain step t of the columns capped at step t-1
-//              (finished by the previous call's resume launch)
-//   caller's:  the main launch of step t, the canopy loop capped, skipping
-//              the columns capped at step t-1
-//   companion: the resume launch of step t for the columns it capped
-// Every column is at step t once both streams are done (nmp_pipe_join).
-int nmp_pipe_step(nmp_pipe* p, int64_t ld, const float zsoil[4], float dt, float julian,
-                  int32_t yearlen, void* state, int32_t* isnow, const void* static_f,
-                  const int32_t* static_i, const void* forcing, void* diag, int diag_level,
-                  int32_t* col_status) {
-  if (!p) return NMP_E_ARG;
-  nmp_engine* e = p->eng;
-  if (!julian_ok(julian, yearlen)) return NMP_E_CALENDAR;
-  int rc = check_common(e, p->ncol, ld, zsoil, dt, yearlen, state, isnow, static_f, static_i,
-                        forcing, diag, diag_level, col_status);
-  if (rc != NMP_OK) return rc;
-  if (p->state && p->state != state) return NMP_E_ARG;  // one column set per pipeline
-  p->state = state;
-  if (!p->capped) {  // no cap in force: plain steps on the caller's stream
-    rc = launch(e, p->ncol, ld, zsoil, dt, julian, yearlen, state, isnow, static_f, static_i,
-                forcing, diag, diag_level, col_status, p->s);
-    if (rc == NMP_OK) ++p->t;
-    return rc;
-  }
-  nmp::KArgs<float> a;
-  fill_args(a, e, p->ncol, ld, zsoil, dt, julian, yearlen, state, isnow, static_f, static_i,
-            forcing, diag, diag_level, col_status, nullptr, nullptr, nullptr);
-  const int par = (int)(p->t & 1), prev = par ^ 1;
-  a.cap_k = p->cap_k;
-  a.cap_ld = p->ncol;
-  a.cap_step_of = p->step_of;
-  a.cap_step = (int32_t)(p->t & 0x3fffffff);
-  a.cap_skip = p->t == 0 ? -1 : (int32_t)((p->t - 1) & 0x3fffffff);
-  auto ok = [](hipError_t x) { return x == hipSuccess; };
-  // (1) companion: step t of the previous step's capped columns, after
-  // everything the caller enqueued for this step (its forcing, for one)
-  if (p->t > 0) {
-    a.cap_count = p->count[prev];
-    a.cap_list = p->list[prev];
-    a.cap_ctx = p->ctx[prev];
-    if (!ok(hipEventRecord(p->e_entry, p->s)) || !ok(hipStreamWaitEvent(p->rs, p->e_entry, 0)) ||
-        !ok(nmp::launch_sflx<float, true>(e->dparams, a, p->rs, false, e->os, nmp::kModeListed)) ||
-        !ok(hipEventRecord(p->e_listed[par], p->rs)))
-      return NMP_E_DEVICE;
-  }
-  // (2) caller's stream, once the companion's step t-1 of the columns capped
-  // at t-2 is done (their state, and list parity t free again): the main
-  // launch of step t, skipping the columns capped at t-1
-  a.cap_count = p->count[par];
-  a.cap_list = p->list[par];
-  a.cap_ctx = p->ctx[par];
-  if (!ok(hipStreamWaitEvent(p->s, p->e_listed[prev], 0)) ||
-      !ok(hipMemsetAsync(p->count[par], 0, sizeof(int32_t), p->s)) ||
-      !ok(nmp::launch_sflx<float, true>(e->dparams, a, p->s, false, e->os, nmp::kModeCapped)) ||
-      !ok(hipEventRecord(p->e_main, p->s)))
-    return NMP_E_DEVICE;
-  // (3) companion: the resume launch of step t
-  if (!ok(hipStreamWaitEvent(p->rs, p->e_main, 0)) ||
-      !ok(nmp::launch_sflx<float, true>(e->dparams, a, p->rs, false, e->os, nmp::kModeResume)))
-    return NMP_E_DEVICE;
-  ++p->t;
-  return NMP_OK;
-}
-
-// Make `stream` wait until every column of the pipeline has completed the
-// last step issued (the caller's stream and the companion both done).
-int nmp_pipe_join(nmp_pipe* p, void* stream) {
-  if (!p) return NMP_E_ARG;
-  hipStream_t x = static_cast<hipStream_t>(stream);
-  if (hipEventRecord(p->e_rs, p->rs) != hipSuccess || hipStreamWaitEvent(x, p->e_rs, 0) != hipSuccess)
-    return NMP_E_DEVICE;
-  if (x != p->s && (hipEventRecord(p->e_entry, p->s) != hipSuccess ||
-                    hipStreamWaitEvent(x, p->e_entry, 0) != hipSuccess))
-    return NMP_E_DEVICE;
-  return NMP_OK;
-}
-
-// The companion stream, for callers that order their own work after the
-// pipeline's (e.g. a collective reading the step's diagnostics).
-void* nmp_pipe_stream(nmp_pipe* p) { return p ? (void*)p->rs : nullptr; }
-
-void nmp_pipe_destroy(nmp_pipe* p) {
-  if (!p) return;
-  ensure_device(p->eng->device);
-  if (p->rs) (void)hipStreamSynchronize(p->rs);
-  if (p->s) (void)hipStreamSynchronize(p->s);
-  for (int k = 0; k < 2; ++k) {
-    if (p->count[k]) (void)hipFree(p->count[k]);
-    if (p->list[k]) (void)hipFree(p->list[k]);
-    if (p->ctx[k]) (void)hipFree(p->ctx[k]);
-  }
-  if (p->step_of) (void)hipFree(p->step_of);
-  for (hipEvent_t ev : {p->e_entry, p->e_main, p->e_rs, p->e_listed[0], p->e_listed[1]})
-    if (ev) (void)hipEventDestroy(ev);
-  if (p->rs && p->own_rs) (void)hipStreamDestroy(p->rs);
-  delete p;
 }
 
 int nmp_step_binned(nmp_engine* eng, int64_t ncol, int64_t ld, const float zsoil[4], float dt,
@@ -605,6 +373,18 @@ int nmp_forcing_synth(nmp_engine* eng, int64_t ncol, int64_t ld, const void* cli
   return nmp::launch_forcing_synth(eng->precision, ncol, ld, climate, julian, yearlen, seed, step,
                                    first_col, forcing, static_cast<hipStream_t>(stream)) ==
                  hipSuccess
+             ? NMP_OK
+             : NMP_E_DEVICE;
+}
+
+int nmp_forcing_from_ldasin(nmp_engine* eng, int64_t ncol, int64_t ld, const float* ldasin,
+                            void* forcing, void* stream) {
+  if (!eng || ncol < 0 || ld < ncol || ld >= kMaxColumns) return NMP_E_ARG;
+  if (ncol == 0) return NMP_OK;
+  if (!ldasin || !forcing) return NMP_E_ARG;
+  if (ensure_device(eng->device) != NMP_OK) return NMP_E_DEVICE;
+  return nmp::launch_forcing_ldasin(eng->precision, ncol, ld, ldasin, forcing,
+                                    static_cast<hipStream_t>(stream)) == hipSuccess
              ? NMP_OK
              : NMP_E_DEVICE;
 }
@@ -957,14 +737,6 @@ void nmp_finalize(nmp_engine* eng) {
     (void)hipStreamDestroy(eng->hstream);
   }
   if (eng->scratch) hipFree(eng->scratch);
-  if (!eng->cap_bufs.empty()) {
-    (void)hipDeviceSynchronize();  // the launches that used the side buffers
-    for (auto& kv : eng->cap_bufs) {
-      if (kv.second.count) (void)hipFree(kv.second.count);
-      if (kv.second.list) (void)hipFree(kv.second.list);
-      if (kv.second.ctx) (void)hipFree(kv.second.ctx);
-    }
-  }
   if (eng->dparams) hipFree(eng->dparams);
   delete eng;
 }

@@ -47,40 +47,20 @@ struct KArgs {
   // columns stepped per 64-lane wave (8..64, a multiple of 8): below 64 the
   // launch spreads a small column set over more waves (small-N latency hiding)
   int cpw;
-  // Cap and resume of the canopy Newton loop (sflx_kernel.hip, DESIGN.md
-  // "Cap and resume"): in the main launch a lane still iterating after cap_k
-  // iterations appends its column (cap_list) and its loop context (cap_ctx,
-  // [field][slot] with cap_ld slots) at slot atomicAdd(cap_count) and leaves
-  // the step; the resume launch steps the cap_count listed columns on from
-  // that context.  cap_k = 0: no cap.
-  int cap_k;
-  int32_t* cap_count;
-  int32_t* cap_list;
-  T* cap_ctx;
-  int64_t cap_ld;
-  // the deferred pipeline (nmp_pipe_step): the main launch of step
-  // cap_step skips the columns capped at step cap_skip (cap_step_of[c] ==
-  // cap_skip; the companion stream steps them) and records cap_step in
-  // cap_step_of[c] for the columns it caps.  NULL: no skipping.
-  int32_t* cap_step_of;
-  int32_t cap_step, cap_skip;
 };
-
-// launch modes of the step kernel: plain, main launch with the loop capped,
-// resume launch of the capped columns, and a plain step of listed columns
-// (the deferred pipeline's step of the previous step's capped columns)
-enum { kModePlain = 0, kModeCapped = 1, kModeResume = 2, kModeListed = 3 };
-// loop-context fields a capped lane saves (sflx_kernel.hip vege_loop)
-constexpr int kCapFields = 31;
 
 template <class T, bool R>
 hipError_t launch_sflx(const DevParams* dparams, const KArgs<T>& a, hipStream_t stream,
-                       bool small, int os, int mode = kModePlain);
+                       bool small, int os);
 
 // csrc/forcing.hip: synthetic forcing of one step from the climate records
 hipError_t launch_forcing_synth(int precision, int64_t ncol, int64_t ld, const void* clim,
                                 double julian, int32_t yearlen, uint64_t seed, int64_t step,
                                 int64_t first_col, void* out, hipStream_t stream);
+
+// csrc/forcing.hip: the 12 forcing fields from the LDASIN block (fp32)
+hipError_t launch_forcing_ldasin(int precision, int64_t ncol, int64_t ld, const float* in,
+                                 void* out, hipStream_t stream);
 
 // csrc/routines.hip: the reference's public routines frh2o / calhum over n
 // elements (device pointers, engine precision; math 0 = the fp32 "ref" policy)

@@ -883,7 +883,6 @@ struct Sink {
   uint8_t* cost;      // cost key (re-binning), or NULL
   const T* fice;      // caller FICEOLD, or NULL
   int64_t col;        // this lane's column
-  int64_t cap_slot;   // (kModeResume) the column's slot in the cap side buffer
   template <class E>
   DEV E* at(E* base, int f) const { return col_at(base, ld, col, f); }
   // late loads: fields first needed deep in the step are read there, not at
@@ -1020,10 +1019,6 @@ static __device__ unsigned int nmp_fb_reason[32];
 #ifndef NMP_VEGE_UNROLL
 #define NMP_VEGE_UNROLL 1
 #endif
-// NMP_CAP_RESUME=0: build without the cap and resume kernels (sflx_kargs.h)
-#ifndef NMP_CAP_RESUME
-#define NMP_CAP_RESUME 1
-#endif
 // NMP_SKIP_2M=0: the 2-m diagnostic chain also on steps without diagnostics (A/B)
 #ifndef NMP_SKIP_2M
 #define NMP_SKIP_2M 1
@@ -1069,11 +1064,7 @@ constexpr Opt kOptionSet[3] = {{1, 1, 1, 1, 1, 1, 1, 1, 2, 1, 1, 1},
                                {1, 1, 1, 1, 1, 1, 1, 1, 2, 1, 1, 1},
                                {2, 1, 1, 1, 1, 1, 1, 1, 2, 1, 1, 1}};
 
-// MODE (sflx_kargs.h): kModePlain; kModeCapped, the main launch of the cap
-// and resume split (a lane still in the canopy Newton loop after A.cap_k
-// iterations saves its loop context and leaves the step); kModeResume, the
-// launch that steps those columns on from their context.
-template <class T, bool R, int OS, int MODE = kModePlain>
+template <class T, bool R, int OS>
 DEV void sflx_column(const DevParams& P, const KArgs<T>& A, Col<T>& c, const Sink<T>& out) {
   typedef Mth<T, R> M;
 
@@ -1251,11 +1242,9 @@ DEV void sflx_column(const DevParams& P, const KArgs<T>& A, Col<T>& c, const Sin
       rho[ib] = rmax((T)V.rhol[ib] * wl + (T)V.rhos[ib] * ws, mpe6);
       tau[ib] = rmax((T)V.taul[ib] * wl + (T)V.taus[ib] * ws, mpe6);
     }
-    // snowage: func.f90:2008-2054.  A resumed column's TAUSS (and ALBOLD below)
-    // were advanced and stored by the main launch before the loop: used as read
+    // snowage: func.f90:2008-2054
     T fage;
-    if (MODE == kModeResume) {
-    } else if (c.sneqv <= L(0.0)) {
+    if (c.sneqv <= L(0.0)) {
       c.tauss = L(0.0);
     } else if (c.sneqv > L(800.0)) {
       c.tauss = L(0.0);
@@ -1285,12 +1274,9 @@ DEV void sflx_column(const DevParams& P, const KArgs<T>& A, Col<T>& c, const Sin
     }
     if (o.alb == 2) {  // snowalb_class: func.f90:2105-2151
       const T decay = (sizeof(T) == 4 && R) ? (T)A.c_albdecay : M::exp(-L(0.01) * DT / L(3600.0));
-      T alb = c.albold;
-      if (MODE != kModeResume) {
-        alb = L(0.55) + (c.albold - L(0.55)) * decay;
-        if (c.qsnow > L(0.0))
-          alb = alb + rmin(c.qsnow * DT, (T)P.g.swemax) * (L(0.84) - alb) / (T)P.g.swemax;
-      }
+      T alb = L(0.55) + (c.albold - L(0.55)) * decay;
+      if (c.qsnow > L(0.0))
+        alb = alb + rmin(c.qsnow * DT, (T)P.g.swemax) * (L(0.84) - alb) / (T)P.g.swemax;
       albsnd[0] = albsnd[1] = albsni[0] = albsni[1] = alb;
       c.albold = alb;
     }
@@ -1323,10 +1309,8 @@ DEV void sflx_column(const DevParams& P, const KArgs<T>& A, Col<T>& c, const Sin
     fsun = (L(1.0) - M::exp(-ext * vaia)) / rmax(ext * vaia, mpe6);
     ext = fsun;
     fsun = (ext < L(0.01)) ? L(0.) : ext;
-    if (MODE != kModeResume) {
-      out.s(NMP_S_ALBOLD, c.albold);
-      out.s(NMP_S_TAUSS, c.tauss);
-    }
+    out.s(NMP_S_ALBOLD, c.albold);
+    out.s(NMP_S_TAUSS, c.tauss);
   }
   T fsha = L(1.0) - fsun;
   T laisun = elai * fsun;
@@ -1460,7 +1444,6 @@ DEV void sflx_column(const DevParams& P, const KArgs<T>& A, Col<T>& c, const Sin
   // ---- vege_flux: func.f90:2465-2964 ----
   T tgv = L(0.0), cmv = L(0.0);
   int vtrips = 0;
-  bool vcapped = false;  // (kModeCapped) this lane left the step at the loop's cap
   if (veg && fveg > L(0.0)) {
     tgv = c.tg;
     const T mpe = L(1E-6);
@@ -1524,11 +1507,8 @@ DEV void sflx_column(const DevParams& P, const KArgs<T>& A, Col<T>& c, const Sin
     // The whole canopy Newton loop (loop1, func.f90:2744-2877) with the
     // division policy `d` (sflx_math.h): every loop variable starts here, so a
     // lane can run it again with the reference's divisions.
-    // rs (std::bool_constant): the resume launch continues a capped lane from
-    // the loop context the main launch saved (cap and resume, below)
-    auto vege_loop = [&](auto& d, auto rs) -> bool {
+    auto vege_loop = [&](auto& d) -> bool {
       constexpr bool kFast = !std::is_same<std::decay_t<decltype(d)>, DivRef<T>>::value;
-      constexpr bool kResume = decltype(rs)::value;
       // CTR, TR and DTV keep IEEE division under every policy: their
       // numerators are products of several possibly small factors, outside
       // what the range proof bounds (tools/div_proof.py)
@@ -1674,80 +1654,17 @@ DEV void sflx_column(const DevParams& P, const KArgs<T>& A, Col<T>& c, const Sin
         c.qsfc = d.div(L(0.622) * c.eah, d.rec(c.sfcprs - L(0.378) * c.eah));
         return dtv;
       };
-      // Cap and resume: the loop context at the top of an iteration -- every
-      // value an iteration reads from the ones before it, and the loop's
-      // outputs -- as one list for the save and the restore
-      auto ctx = [&](auto&& f) {
-        f(0, c.tv); f(1, c.tah); f(2, c.eah); f(3, c.qsfc); f(4, fv); f(5, h); f(6, hg);
-        f(7, moz); f(8, fm); f(9, fh); f(10, fm2); f(11, fh2); f(12, fhg); f(13, wstar);
-        f(14, rahg); f(15, rb); f(16, rahc); f(17, cah); f(18, cvh); f(19, cmv); f(20, chv);
-        f(21, irc); f(22, shc); f(23, evc); f(24, tr); f(25, rssun); f(26, rssha);
-        f(27, psnsun); f(28, psnsha);
-      };
-      static_assert(kCapFields == 31, "29 reals + MOZSGN + LITER");
-      int iter0 = 2;
-      if constexpr (kResume) {
-        // the capped lane's context, saved at the top of iteration cap_k + 1
-        const int64_t slot = out.cap_slot;
-        ctx([&](int f, T& v) { v = A.cap_ctx[f * A.cap_ld + slot]; });
-        mozsgn = (int)A.cap_ctx[29 * A.cap_ld + slot];  // small integers: exact as reals
-        liter = (int)A.cap_ctx[30 * A.cap_ld + slot];
-        iter0 = A.cap_k + 1;
-      } else {
-        if constexpr (kFast) NMP_DOM(ok, 18, in(c.tv, (T)NMP_DOM_T_LO, (T)NMP_DOM_T_HI));
-        vtrips = 1;
-        vege_iter(1, std::true_type{});  // iter 1 cannot exit (the test needs iter >= 5)
-      }
+      if constexpr (kFast) NMP_DOM(ok, 18, in(c.tv, (T)NMP_DOM_T_LO, (T)NMP_DOM_T_HI));
+      vtrips = 1;
+      vege_iter(1, std::true_type{});  // iter 1 cannot exit (the test needs iter >= 5)
       NMP_UNROLL(NMP_VEGE_UNROLL)
-      for (int iter = iter0; iter <= 20; ++iter) {
-        if constexpr (MODE == kModeCapped && kFast && !kResume) {
-          // A lane still iterating after cap_k iterations leaves the loop
-          // here, before iteration cap_k + 1 (lanes already outside the range
-          // proof's window keep going to their IEEE re-run)
-          if (iter > A.cap_k && ok) {
-            vcapped = true;
-            break;
-          }
-        }
-#ifdef NMP_VEGE_CAP_PROBE
-        // (timing probe only, results wrong for capped lanes) a lane still
-        // iterating after NMP_VEGE_CAP_PROBE iterations leaves the step here:
-        // the main launch of a "cap and resume" split without its side buffer
-        if (kFast && iter > NMP_VEGE_CAP_PROBE) {
-          vcapped = true;
-          break;
-        }
-#endif
+      for (int iter = 2; iter <= 20; ++iter) {
         vtrips = iter;
         if constexpr (kFast) NMP_DOM(ok, 19, in(c.tv, (T)NMP_DOM_T_LO, (T)NMP_DOM_TV_HI));
         const T dtv = vege_iter(iter, std::false_type{});
         if (liter == 1) break;
         if (iter >= 5 && fabs(dtv) <= L(0.01) && liter == 0) liter = 1;
       }
-#ifdef NMP_VEGE_CAP_PROBE
-      if (vcapped) return false;
-#else
-      if constexpr (MODE == kModeCapped && kFast && !kResume) {
-        if (vcapped) {
-          // the capped lane's column and loop context go to the next free
-          // slots of the side buffer (one atomic per wave); its step goes on
-          // in the resume launch
-          const uint64_t m = __builtin_amdgcn_read_exec();
-          const int rank = (int)__builtin_amdgcn_mbcnt_hi(
-              (uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-          int base = 0;
-          if (rank == 0) base = atomicAdd(A.cap_count, (int)__builtin_popcountll(m));
-          base = __shfl(base, (int)__builtin_ctzll(m));
-          T* const cp = A.cap_ctx + (base + rank);
-          ctx([&](int f, T& v) { cp[f * A.cap_ld] = v; });
-          cp[29 * A.cap_ld] = (T)mozsgn;
-          cp[30 * A.cap_ld] = (T)liter;
-          A.cap_list[base + rank] = (int32_t)out.col;  // this column
-          if (A.cap_step_of) A.cap_step_of[out.col] = A.cap_step;
-          return false;
-        }
-      }
-#endif
       return ok;
     };
     DivRef<T> dr;
@@ -1759,12 +1676,10 @@ DEV void sflx_column(const DevParams& P, const KArgs<T>& A, Col<T>& c, const Sin
       DivFast32 df;
 #ifdef NMP_VD_NOFALLBACK
       (void)vege_domain_ok();
-      vege_loop(df, std::false_type{});
+      vege_loop(df);
       if (false) {  // (timing probe only: not exact in general)
 #else
-      if (!vege_domain_ok() || !vege_loop(df, std::bool_constant<MODE == kModeResume>{})) {
-        // a capped lane's step continues in the resume launch
-        if (vcapped) return;
+      if (!vege_domain_ok() || !vege_loop(df)) {
 #endif
 #ifdef NMP_COUNT_FALLBACK
         atomicAdd(&nmp_fallback_ctr, 1u);
@@ -1774,13 +1689,13 @@ DEV void sflx_column(const DevParams& P, const KArgs<T>& A, Col<T>& c, const Sin
         c.tv = out.ls(NMP_S_TV);
         c.tah = out.ls(NMP_S_TAH);
         c.eah = out.ls(NMP_S_EAH);
-        vege_loop(dr, std::false_type{});
+        vege_loop(dr);
       }
     } else {
-      vege_loop(dr, std::false_type{});
+      vege_loop(dr);
     }
 #else
-    vege_loop(dr, std::false_type{});
+    vege_loop(dr);
 #endif
     // under-canopy fluxes and TG (loop2, :2881-2914)
     air = -emg * (L(1.0) - emv) * c.lwdn - emg * emv * SB * p4(c.tv);
@@ -3222,7 +3137,7 @@ DEV void lds_copy_wait() {
 #define NMP_LOAD_COLUMN(T, R)                                                                \
   Col<T> c;                                                                                  \
   const Sink<T> out{a.diag, a.state, a.ld, a.diag_level, a.static_f, a.static_i, a.forcing,  \
-                    a.isnow, a.cost, a.ficeold, c0, gid};                                    \
+                    a.isnow, a.cost, a.ficeold, c0};                                         \
   c.tv = out.ls(NMP_S_TV); c.tg = out.ls(NMP_S_TG);                                          \
   c.fwet = out.ls(NMP_S_FWET); c.snowh = out.ls(NMP_S_SNOWH);                                \
   c.sneqv = out.ls(NMP_S_SNEQV);                                                             \
@@ -3263,20 +3178,11 @@ DEV void lds_copy_wait() {
     }                                                                                        \
   }
 
-template <class T, bool R, bool SMALL, int OS, int MODE = kModePlain>
+template <class T, bool R, bool SMALL, int OS>
 __global__ __launch_bounds__(NMP_BLOCK)
 __attribute__((amdgpu_waves_per_eu(waves_per_eu<T>(SMALL))))
 void sflx_step_kernel(const DevParams* __restrict__ gparams,
                                                           KArgs<T> a) {
-  // the resume launch has the main launch's grid; only the first blocks hold
-  // listed columns, the others leave before staging the tables
-  // resume / listed launches: lane gid steps the gid-th listed column
-  constexpr bool kListed = MODE == kModeResume || MODE == kModeListed;
-  int64_t nres = 0;
-  if constexpr (kListed) {
-    nres = *a.cap_count;
-    if ((int64_t)blockIdx.x * NMP_BLOCK >= nres) return;
-  }
 #ifdef NMP_WAVE_TIMING
   const unsigned long long wt0 = __builtin_amdgcn_s_memrealtime();
 #endif
@@ -3307,21 +3213,16 @@ void sflx_step_kernel(const DevParams* __restrict__ gparams,
   const int lane = threadIdx.x & 63;
   if (lane >= a.cpw) return;
   const int64_t gid = (blk * (NMP_BLOCK / 64) + (threadIdx.x >> 6)) * a.cpw + lane;
-  if (gid >= (kListed ? nres : a.ncol)) return;
+  if (gid >= a.ncol) return;
   // re-binned launch: this lane steps column order[gid] (a permutation of the
-  // columns; every column is independent, so results do not depend on it);
-  // resume / listed launch: the gid-th capped column
-  const int64_t c0 = kListed ? (int64_t)a.cap_list[gid] : a.order ? (int64_t)a.order[gid] : gid;
-  // the deferred pipeline's main launch: the previous step's capped columns
-  // are stepped on the companion stream
-  if constexpr (MODE == kModeCapped)
-    if (a.cap_step_of && a.cap_step_of[c0] == a.cap_skip) return;
+  // columns; every column is independent, so results do not depend on it)
+  const int64_t c0 = a.order ? (int64_t)a.order[gid] : gid;
   const T* st0 = a.state + c0;
   // layer state: through the LDS copy (kPrefetch) or straight from HBM.  The
   // copy is issued first; the column's other fields load while it is in flight
   if constexpr (kPrefetch<T, R>) copy_layers_to_lds(st0, a.ld);
   NMP_LOAD_COLUMN(T, R);
-  sflx_column<T, R, OS, MODE == kModeListed ? kModePlain : MODE>(sp, a, c, out);
+  sflx_column<T, R, OS>(sp, a, c, out);
   if (c.status != 0) *out.at(a.status, 0) |= c.status;
 #ifdef NMP_WAVE_TIMING
   {
@@ -3343,35 +3244,10 @@ void sflx_step_kernel(const DevParams* __restrict__ gparams,
 #endif
 }
 
-// launch wrapper (one instantiation per precision / math policy).  The cap
-// and resume modes exist for the production kernels only: fp32 "ref" math,
-// full occupancy, a compiled option set.
+// launch wrapper of one occupancy instantiation: the kernel of option set os
 template <class T, bool R, bool SMALL>
 void launch_os(int os, dim3 grid, dim3 block, hipStream_t stream, const DevParams* dparams,
-               const KArgs<T>& a, int mode) {
-  if constexpr (sizeof(T) == 4 && R && !SMALL && NMP_CAP_RESUME) {
-    if (mode != kModePlain && os != 0) {
-      if (os == 1 && mode == kModeCapped)
-        hipLaunchKernelGGL((sflx_step_kernel<T, R, SMALL, 1, kModeCapped>), grid, block, 0, stream,
-                           dparams, a);
-      else if (os == 1 && mode == kModeResume)
-        hipLaunchKernelGGL((sflx_step_kernel<T, R, SMALL, 1, kModeResume>), grid, block, 0, stream,
-                           dparams, a);
-      else if (os == 1)
-        hipLaunchKernelGGL((sflx_step_kernel<T, R, SMALL, 1, kModeListed>), grid, block, 0, stream,
-                           dparams, a);
-      else if (mode == kModeCapped)
-        hipLaunchKernelGGL((sflx_step_kernel<T, R, SMALL, 2, kModeCapped>), grid, block, 0, stream,
-                           dparams, a);
-      else if (mode == kModeResume)
-        hipLaunchKernelGGL((sflx_step_kernel<T, R, SMALL, 2, kModeResume>), grid, block, 0, stream,
-                           dparams, a);
-      else
-        hipLaunchKernelGGL((sflx_step_kernel<T, R, SMALL, 2, kModeListed>), grid, block, 0, stream,
-                           dparams, a);
-      return;
-    }
-  }
+               const KArgs<T>& a) {
   if (os == 1)
     hipLaunchKernelGGL((sflx_step_kernel<T, R, SMALL, 1>), grid, block, 0, stream, dparams, a);
   else if (os == 2)
@@ -3386,14 +3262,14 @@ void launch_os(int os, dim3 grid, dim3 block, hipStream_t stream, const DevParam
 // -9 % (profiles/r05/retune_ab.txt)
 #if defined(NMP_TU) && NMP_TU == 8
 extern template void launch_os<double, false, true>(int, dim3, dim3, hipStream_t,
-                                                    const DevParams*, const KArgs<double>&, int);
+                                                    const DevParams*, const KArgs<double>&);
 #endif
 
 // launch wrapper (one instantiation per precision / math policy).  os: the
 // compiled option set matching the engine's options (0 = read at run time)
 template <class T, bool R>
 hipError_t launch_sflx(const DevParams* dparams, const KArgs<T>& a, hipStream_t stream,
-                       bool small, int os, int mode) {
+                       bool small, int os) {
   const int64_t cols_per_block = (int64_t)(NMP_BLOCK / 64) * a.cpw;
   const int64_t grid = (a.ncol + cols_per_block - 1) / cols_per_block;
   const int block = NMP_BLOCK;
@@ -3401,9 +3277,9 @@ hipError_t launch_sflx(const DevParams* dparams, const KArgs<T>& a, hipStream_t 
   // the fast-math fp32 path has neither a small nor option-set instantiation (code size)
   if constexpr (sizeof(T) == 8 || R) {
     if (small)
-      launch_os<T, R, true>(os, dim3((unsigned)grid), dim3(block), stream, dparams, a, kModePlain);
+      launch_os<T, R, true>(os, dim3((unsigned)grid), dim3(block), stream, dparams, a);
     else
-      launch_os<T, R, false>(os, dim3((unsigned)grid), dim3(block), stream, dparams, a, mode);
+      launch_os<T, R, false>(os, dim3((unsigned)grid), dim3(block), stream, dparams, a);
   } else {
     hipLaunchKernelGGL((sflx_step_kernel<T, R, false, 0>), dim3((unsigned)grid), dim3(block), 0,
                        stream, dparams, a);
@@ -3495,17 +3371,17 @@ extern "C" long long nmp_debug_wave_records(unsigned long long* out, long long m
 // with its own flags; without NMP_TU one object holds them all.
 #if !defined(NMP_TU) || NMP_TU == 4
 template hipError_t launch_sflx<float, true>(const DevParams*, const KArgs<float>&, hipStream_t,
-                                             bool, int, int);
+                                             bool, int);
 template hipError_t launch_sflx<float, false>(const DevParams*, const KArgs<float>&, hipStream_t,
-                                              bool, int, int);
+                                              bool, int);
 #endif
 #if !defined(NMP_TU) || NMP_TU == 8
 template hipError_t launch_sflx<double, false>(const DevParams*, const KArgs<double>&, hipStream_t,
-                                               bool, int, int);
+                                               bool, int);
 #endif
 #if defined(NMP_TU) && NMP_TU == 9
 template void launch_os<double, false, true>(int, dim3, dim3, hipStream_t, const DevParams*,
-                                             const KArgs<double>&, int);
+                                             const KArgs<double>&);
 #endif
 
 }  // namespace nmp

@@ -30,12 +30,22 @@ allowed), which writes them for the whole grid.
 
 Forcing reaches the GPU through `ForcingUpload`: pinned, double-buffered
 host buffers copied on a copy stream, so the host builds step t+1's forcing
-while the GPU steps t.
+while the GPU steps t.  From LDASIN files the upload is the files' own
+variables plus COSZ (ncio.LdasinForcing.raw, 36 B per column in fp32), and
+the engine forms the 12 forcing fields on each range's stream right before
+its launch (nmp_forcing_from_ldasin); the 12-field host form (48 B per
+column, 96 in fp64) remains for providers that supply all of them.
+
+`phase_s` accumulates the host time of the loop's parts (forcing provider,
+upload enqueue, launch enqueue, output), for the offline-driver timing
+(tools/offline_timing.py).
 """
 from __future__ import annotations
 
 import datetime
 import os
+import time
+from collections import defaultdict
 
 import numpy as np
 import torch
@@ -68,22 +78,27 @@ class ForcingUpload:
     puts later: the host side waits for b's previous upload to land, the copy
     stream for the launches that read it (`consumed_by`)."""
 
-    def __init__(self, n: int, dtype, device, nbuf: int = 2):
+    def __init__(self, n: int, dtype, device, nbuf: int = 2, nfield: int = L.NFORCING):
         dev = torch.device(device)
-        self.host = [torch.empty((L.NFORCING, n), dtype=dtype, pin_memory=True)
+        self.host = [torch.empty((nfield, n), dtype=dtype, pin_memory=True)
                      for _ in range(nbuf)]
-        self.dev = [torch.empty((L.NFORCING, n), dtype=dtype, device=dev) for _ in range(nbuf)]
+        self.dev = [torch.empty((nfield, n), dtype=dtype, device=dev) for _ in range(nbuf)]
         self.stream = torch.cuda.Stream(dev)
         self.uploaded = [None] * nbuf
         self.consumed = [()] * nbuf
         self.count = 0
 
-    def put(self, f: np.ndarray) -> torch.Tensor:
+    def put(self, f: np.ndarray | None = None, fill=None) -> torch.Tensor:
+        """Upload f, or whatever fill(host_array) writes into the pinned buffer
+        (a provider filling it in place saves a host copy)."""
         b = self.count % len(self.host)
         self.count += 1
         if self.uploaded[b] is not None:
             self.uploaded[b].synchronize()  # pinned buffer b is free again
-        self.host[b].numpy()[...] = f
+        if fill is not None:
+            fill(self.host[b].numpy())
+        else:
+            self.host[b].numpy()[...] = f
         for e in self.consumed[b]:
             self.stream.wait_event(e)
         with torch.cuda.stream(self.stream):
@@ -143,10 +158,12 @@ class OfflineDriver:
     def __init__(self, cfg: Config, cols: cases.ColumnSet, device: int = 0,
                  params: Params | None = None, forcing=None, precision: int = 4,
                  math: str = "ref", zsoil=cases.CASE_NML_ZSOIL, write: bool = True,
-                 streams: int = 2, grid: ncio.Grid | None = None):
+                 streams: int = 2, grid: ncio.Grid | None = None, ldasin_upload: bool = True):
         """cols: this rank's columns (all of them on a single rank); under an
         initialised process group they must be the rank's shard_range block of
-        the global column set."""
+        the global column set.  ldasin_upload: with a provider that has
+        `raw` (LDASIN files), upload the files' variables and form the forcing
+        on the device (False: the 12-field host form, for comparison)."""
         self.cfg = cfg
         self.grid = grid
         self.engine = Engine(params or Params.builtin(), cfg.engine_options(), device, precision,
@@ -179,6 +196,13 @@ class OfflineDriver:
         self.write = write
         self.diag = torch.zeros((L.NDIAG_OUT, self.cs.ncol), dtype=self.dtype, device=self.dev)
         self.upload = ForcingUpload(self.cs.ncol, self.dtype, self.dev)
+        self.raw_upload = None
+        if ldasin_upload and hasattr(self.forcing, "raw") and self.dev_forcing is None:
+            self.raw_upload = ForcingUpload(self.cs.ncol, torch.float32, self.dev,
+                                            nfield=L.NLDASIN)
+            self.raw_fbuf = torch.empty((2, L.NFORCING, self.cs.ncol), dtype=self.dtype,
+                                        device=self.dev)
+        self.phase_s = defaultdict(float)
         self.gather = None
         if dist.is_initialized():
             self.gather = shard.DiagGather(L.NDIAG_OUT, total, self.dtype, self.dev, dst=0)
@@ -191,7 +215,7 @@ class OfflineDriver:
     @classmethod
     def from_files(cls, cfg: Config, device: int = 0, params: Params | None = None,
                    init: str | None = None, order: str | None = "lon-snow-type",
-                   **kw) -> "OfflineDriver":
+                   host_threads: int | None = None, **kw) -> "OfflineDriver":
         """The run the namelist describes: static file (cfg.constfile), initial
         state (cfg.initfile, or `init`) and LDASIN forcing (cfg.indir every
         cfg.input_frequency), netCDF-3 files in the layouts of ncio.py.
@@ -199,7 +223,9 @@ class OfflineDriver:
         order: the land points are laid out in the engine in this coherent
         order (order.coherent_order; None = grid order).  The permutation is
         applied when columns are read from the files and undone when they are
-        written, so files always hold the grid."""
+        written, so files always hold the grid.
+        host_threads: threads that build each step's forcing on the host
+        (ncio.LdasinForcing; default NMP_HOST_THREADS, else 8)."""
         P = params or Params.builtin()
         grid, sf, si = ncio.read_static(cfg.constfile, P.as_dict(), cfg.begdatetime)
         st, isn, t0, step = ncio.read_state(init or cfg.initfile, grid)
@@ -212,7 +238,7 @@ class OfflineDriver:
         cols = cases.ColumnSet(sf[:, idx], si[:, idx], st[:, idx], isn[idx], grid.lon_rad[idx],
                                *([None] * 6))
         forcing = ncio.LdasinForcing(cfg.indir, grid, cfg.begdatetime, cfg.input_interval,
-                                     cols=idx)
+                                     cols=idx, threads=host_threads)
         drv = cls(cfg, cols, device, P, forcing, grid=grid, **kw)
         drv.t, drv.step_index = t0, step
         drv.perm, drv.cols_index = perm, idx
@@ -275,17 +301,35 @@ class OfflineDriver:
             # restart copies, the gather fence assemble() left there) and, for
             # host forcing, for the upload of this step's buffer
             cur = torch.cuda.current_stream(self.dev)
-            pre, after = None, (cur, self.upload.stream)
-            if self.dev_forcing is not None:
+            pre, after, upload = None, (cur, self.upload.stream), self.upload
+            tp = time.perf_counter()
+            fl = self.forcing.fields(t0) if hasattr(self.forcing, "fields") else None
+            self.phase_s["read"] += time.perf_counter() - tp  # LDASIN files, per input time
+            tp = time.perf_counter()
+            if self.raw_upload is not None and "CO2AIR" not in fl and "O2AIR" not in fl:
+                # the LDASIN block straight into a pinned buffer and up; each
+                # range forms its 12 fields on its own stream before its launch
+                step_k, t_k = self.step_index, t0
+                raw = self.raw_upload.put(fill=lambda h: self.forcing.raw(step_k, t_k, out=h))
+                f = self.raw_fbuf[self.step_index % 2]
+                pre = lambda st, rng: self.engine.forcing_from_ldasin(  # noqa: E731
+                    raw, f, stream=st, cols=rng)
+                after, upload = (cur, self.raw_upload.stream), self.raw_upload
+            elif self.dev_forcing is not None:
                 clim, fbuf = self.dev_forcing
                 f = fbuf[self.step_index % 2]
                 jul, yl, k = timeman.julian(t0), timeman.yearlen(t0.year), self.step_index
                 pre = lambda st, rng: self.engine.forcing_synth(  # noqa: E731
                     clim, jul, yl, self.forcing.seed, k, f, self.forcing.first_col, stream=st,
                     cols=rng)
-                after = cur
+                after, upload = cur, None
+            elif fl is not None:  # LDASIN files, the 12-field form: built into the pinned buffer
+                step_k, t_k = self.step_index, t0
+                f = self.upload.put(fill=lambda h: self.forcing(step_k, t_k, out=h))
             else:
                 f = self.upload.put(self.forcing(self.step_index, t0))
+            self.phase_s["forcing"] += time.perf_counter() - tp
+            tp = time.perf_counter()
             diag = self.diag
             if out and self.gather is not None:
                 b = self.n_out % len(self.gather.bufs)
@@ -294,8 +338,10 @@ class OfflineDriver:
             self.ranges.step(f, self.zsoil, self.dt, timeman.julian(t0), timeman.yearlen(t0.year),
                              diag if out else None, L.DIAG_OUT_LEVEL if out else L.DIAG_NONE,
                              after=after, pre=pre)
-            if self.dev_forcing is None:
-                self.upload.consumed_by(self.ranges.producers)
+            if upload is not None:
+                upload.consumed_by(self.ranges.producers)
+            self.phase_s["launch"] += time.perf_counter() - tp
+            tp = time.perf_counter()
             self.t, self.step_index = t1, self.step_index + 1
             if out:
                 if self.gather is not None:
@@ -316,6 +362,7 @@ class OfflineDriver:
                         np.savez(path, time=np.array(t1.isoformat()),
                                  fields=np.array(",".join(L.DIAG_OUT)), diag=d.cpu().numpy())
                     self.written.append(path)
+            self.phase_s["output"] += time.perf_counter() - tp
             if _is_boundary(t1, cfg.begdatetime, res_every) and self.write:
                 os.makedirs(cfg.resdir, exist_ok=True)
                 name = (f"RESTART.{_stamp(t1)}_DOMAIN1.nc" if self.grid is not None and

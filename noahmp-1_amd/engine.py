@@ -105,19 +105,6 @@ class Engine:
         _lib.check(min(rc, 0), "nmp_set_launch_variant")
         return {i: k for k, i in LAUNCH_VARIANTS.items()}[rc]
 
-    def vege_cap(self, k: int | None = None) -> int:
-        """nmp_set_vege_cap: cap the canopy Newton loop at k iterations and
-        finish the capped columns in a compacted resume launch (2..19, 0 = off;
-        None only queries).  Returns the cap in use.  Results do not depend on it."""
-        rc = self._lib.nmp_set_vege_cap(self._h, -1 if k is None else int(k))
-        _lib.check(min(rc, 0), "nmp_set_vege_cap")
-        return rc
-
-    def pipe(self, cs: ColumnState, stream=None, cols: tuple[int, int] | None = None) -> "CapPipe":
-        """nmp_pipe_create: the deferred cap-and-resume pipeline over cs (or its
-        column range cols=(lo, hi)) stepping on `stream` (default: current)."""
-        return CapPipe(self, cs, stream, cols)
-
     def set_math(self, mode: int):
         _lib.check(self._lib.nmp_set_math(self._h, int(mode)), "nmp_set_math")
         self.math = int(mode)
@@ -231,6 +218,25 @@ class Engine:
                                                int(step), int(first_col) + lo, _ptr(out, lo),
                                                C.c_void_p(s.cuda_stream)), "nmp_forcing_synth")
 
+    def forcing_from_ldasin(self, ldasin: torch.Tensor, out: torch.Tensor, stream=None,
+                            cols: tuple[int, int] | None = None):
+        """nmp_forcing_from_ldasin: the 12 forcing fields of one step into out
+        (NFORCING, n), engine precision, from the (NLDASIN, n) fp32 LDASIN
+        block (layout.LDASIN); SFCPRS, CO2AIR and O2AIR formed on the device
+        from PSFC.  cols=(lo, hi) converts only those columns."""
+        n = int(ldasin.shape[1])
+        lo, hi = (0, n) if cols is None else (int(cols[0]), int(cols[1]))
+        assert 0 <= lo <= hi <= n
+        assert ldasin.shape == (L.NLDASIN, n) and ldasin.dtype == torch.float32
+        assert out.shape == (L.NFORCING, n) and out.dtype == self.dtype
+        assert ldasin.is_contiguous() and out.is_contiguous()
+        for t in (ldasin, out):
+            assert t.device.type == "cuda" and t.device.index == self.device
+        s = stream if stream is not None else torch.cuda.current_stream(self.device)
+        _lib.check(self._lib.nmp_forcing_from_ldasin(self._h, hi - lo, n, _ptr(ldasin, lo),
+                                                     _ptr(out, lo), C.c_void_p(s.cuda_stream)),
+                   "nmp_forcing_from_ldasin")
+
     # ---- the reference's other public routines (nmp_frh2o / nmp_calhum) ------
     def frh2o(self, sltyp, tkelv, smc, sh2o, status=None, stream=None):
         """frh2o (func.f90:4494-4598) elementwise.  Device tensors (engine
@@ -338,58 +344,6 @@ class Engine:
                                          C.c_void_p(s.cuda_stream)), "nmp_run_out")
 
 
-class CapPipe:
-    """nmp_pipe_*: steps one column range through the deferred cap-and-resume
-    pipeline (include/noahmp_engine.h): main launches on `stream`, the resume
-    and listed launches on the pipeline's companion stream (`companion`).
-    After join(s), s is ordered after every column's last step."""
-
-    def __init__(self, engine: Engine, cs: ColumnState, stream=None,
-                 cols: tuple[int, int] | None = None):
-        self.engine, self.cs = engine, cs
-        n = cs.ncol
-        self.lo, self.hi = (0, n) if cols is None else (int(cols[0]), int(cols[1]))
-        assert 0 <= self.lo < self.hi <= n
-        self.stream = stream if stream is not None else torch.cuda.current_stream(engine.device)
-        # the companion is a torch stream, so that its lifetime is torch's: tensors
-        # recorded on it (record_stream) may be freed after the pipeline is gone
-        self.companion = torch.cuda.Stream(self.stream.device)
-        h = C.c_void_p()
-        _lib.check(engine._lib.nmp_pipe_create(engine._h, self.hi - self.lo,
-                                               C.c_void_p(self.stream.cuda_stream),
-                                               C.c_void_p(self.companion.cuda_stream),
-                                               C.byref(h)), "nmp_pipe_create")
-        self._h = h
-
-    def step(self, forcing: torch.Tensor, zsoil, dt: float, julian: float, yearlen: int,
-             diag: torch.Tensor | None = None, diag_level: int = L.DIAG_NONE):
-        cs, lo, n = self.cs, self.lo, self.cs.ncol
-        self.engine._check_cols(cs, forcing)
-        if diag_level != L.DIAG_NONE:
-            assert diag is not None and diag.is_contiguous() and diag.shape[-1] == n
-        zs = (C.c_float * 4)(*[float(z) for z in zsoil])
-        _lib.check(self.engine._lib.nmp_pipe_step(
-            self._h, n, zs, float(dt), float(julian), int(yearlen), _ptr(cs.state, lo),
-            _ptr(cs.isnow, lo), _ptr(cs.static_f, lo), _ptr(cs.static_i, lo), _ptr(forcing, lo),
-            _ptr(diag, lo), int(diag_level), _ptr(cs.status, lo)), "nmp_pipe_step")
-
-    def join(self, stream=None):
-        s = stream if stream is not None else torch.cuda.current_stream(self.engine.device)
-        _lib.check(self.engine._lib.nmp_pipe_join(self._h, C.c_void_p(s.cuda_stream)),
-                   "nmp_pipe_join")
-
-    def close(self):
-        if getattr(self, "_h", None):
-            self.engine._lib.nmp_pipe_destroy(self._h)
-            self._h = None
-
-    def __del__(self):
-        try:
-            self.close()
-        except Exception:
-            pass
-
-
 class StreamShards:
     """Steps one ColumnState as `nshards` column ranges, each on its own HIP stream.
 
@@ -402,8 +356,7 @@ class StreamShards:
 
     def __init__(self, engine: Engine, cs: ColumnState, nshards: int = 2, device=None,
                  rebin_tile: int = 0, rebin_every: int = 1, launch_cols: int = 0,
-                 first_frac: float | None = None, stagger: bool = False,
-                 cap_pipeline: bool = True):
+                 first_frac: float | None = None, stagger: bool = False):
         """rebin_tile > 0 turns on column re-binning (nmp_step_binned /
         nmp_rebin): every `rebin_every` steps each range re-sorts its columns
         within tiles of rebin_tile columns by the trip counts the previous step
@@ -413,10 +366,7 @@ class StreamShards:
         first_frac (two ranges only): the first range's share of the columns
         (default: equal ranges).  stagger: the first step of range i > 0 starts
         after range i - 1's first launch, so the ranges run out of phase (their
-        launches' ramp and drain fall on the other range's full waves).
-        cap_pipeline=False (with the cap on): each range's capped launch and
-        its resume launch run on the range's own stream (nmp_step) instead of
-        the deferred pipeline."""
+        launches' ramp and drain fall on the other range's full waves)."""
         n = cs.ncol
         nshards = max(1, min(int(nshards), max(n, 1)))
         self.engine, self.cs = engine, cs
@@ -428,16 +378,6 @@ class StreamShards:
             self.ranges = [(0, cut), (cut, n)]
         self.rebin_tile, self.rebin_every, self.nstep = int(rebin_tile), max(1, int(rebin_every)), 0
         self.launch_cols = int(launch_cols)
-        # the canopy loop's cap in force: each range steps through its own
-        # deferred cap-and-resume pipeline (CapPipe); its companion stream is
-        # one more producer of the range's results
-        self.pipes = None
-        if engine.precision == 4 and engine.vege_cap() > 0 and not self.rebin_tile \
-                and not self.launch_cols and cap_pipeline:
-            self.pipes = [CapPipe(engine, cs, st, rng if len(self.streams) > 1 else None)
-                          for st, rng in zip(self.streams, self.ranges) if rng[1] > rng[0]]
-            if len(self.pipes) != len(self.streams):
-                self.pipes = None
         self.stagger, self._stag_ev = bool(stagger), None
         assert not (self.launch_cols and self.rebin_tile), "launch_cols: plain launches only"
         self.order = self.cost = None
@@ -468,11 +408,9 @@ class StreamShards:
             if after is not None:
                 for a in after:
                     st.wait_stream(a)
-                users = [st] + ([self.pipes[i].companion] if self.pipes is not None else [])
-                for u in users:
-                    forcing.record_stream(u)
-                    if diag is not None:
-                        diag.record_stream(u)
+                forcing.record_stream(st)
+                if diag is not None:
+                    diag.record_stream(st)
             if self.stagger and self.nstep == 0 and i > 0:
                 st.wait_event(self._stag_ev)
             if pre is not None:
@@ -481,9 +419,7 @@ class StreamShards:
                 events[i][0].record(st)
             if self.rebin_tile and self.nstep > 0 and self.nstep % self.rebin_every == 0:
                 self.engine.rebin(self.cost, self.order, self.rebin_tile, stream=st, cols=rng)
-            if self.pipes is not None:
-                self.pipes[i].step(forcing, zsoil, dt, julian, yearlen, diag, diag_level)
-            elif self.launch_cols:
+            if self.launch_cols:
                 for lo in range(rng[0], rng[1], self.launch_cols):
                     self.engine.step(self.cs, forcing, zsoil, dt, julian, yearlen, diag,
                                      diag_level, stream=st,
@@ -501,9 +437,8 @@ class StreamShards:
 
     @property
     def producers(self):
-        """Every stream that writes the ranges' state and diagnostics (the range
-        streams, and the cap pipelines' companions)."""
-        return self.streams + ([p.companion for p in self.pipes] if self.pipes else [])
+        """Every stream that writes the ranges' state and diagnostics."""
+        return list(self.streams)
 
     def join(self, stream: torch.cuda.Stream | None = None):
         """Make `stream` (default: the current stream) wait for every range."""

@@ -139,6 +139,10 @@ STATE_OFF, NSTATE = _offsets(STATE_FIELDS)
 assert NSTATE == 56
 NSTATIC_F = len(STATIC_F)
 NSTATIC_I = len(STATIC_I)
+# LDASIN block of nmp_forcing_from_ldasin (NMP_L_*): the 8 variables of an
+# LDASIN file (ncio.py) plus the step's COSZ, fp32
+LDASIN = ["T2D", "Q2D", "U2D", "V2D", "PSFC", "RAINRATE", "SWDOWN", "LWDOWN", "COSZ"]
+NLDASIN = len(LDASIN)
 NFORCING = len(FORCING)
 # climate record of the device forcing generator (NMP_CLIM_*, nmp_forcing_synth)
 CLIMATE = ["LAT", "LON", "T0", "AMP", "RH", "PRES", "WIND_U", "WIND_V", "WET"]

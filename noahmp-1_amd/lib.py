@@ -98,6 +98,7 @@ def load(build_if_missing: bool = False):
     lib.nmp_rebin.argtypes = [vp, C.c_int64, vp, vp, C.c_int32, vp]
     lib.nmp_forcing_synth.argtypes = [vp, C.c_int64, C.c_int64, vp, C.c_double, C.c_int32,
                                       C.c_uint64, C.c_int64, C.c_int64, vp, vp]
+    lib.nmp_forcing_from_ldasin.argtypes = [vp, C.c_int64, C.c_int64, vp, vp, vp]
     lib.nmp_run.argtypes = [vp, C.c_int64, C.c_int64, f32p, C.c_float, C.c_float, C.c_int32,
                             C.c_int32, vp, vp, vp, vp, vp, C.c_int64, C.c_int32, vp, C.c_int, vp,
                             vp]
@@ -111,15 +112,6 @@ def load(build_if_missing: bool = False):
     lib.nmp_sflx_column.argtypes = [vp, vp]
     lib.nmp_option_set.argtypes = [vp, C.c_int]
     lib.nmp_set_launch_variant.argtypes = [vp, C.c_int]
-    lib.nmp_set_vege_cap.argtypes = [vp, C.c_int]
-    lib.nmp_pipe_create.argtypes = [vp, C.c_int64, vp, vp, C.POINTER(vp)]
-    lib.nmp_pipe_step.argtypes = [vp, C.c_int64, f32p, C.c_float, C.c_float, C.c_int32, vp, vp,
-                                  vp, vp, vp, vp, C.c_int, vp]
-    lib.nmp_pipe_join.argtypes = [vp, vp]
-    lib.nmp_pipe_stream.argtypes = [vp]
-    lib.nmp_pipe_stream.restype = vp
-    lib.nmp_pipe_destroy.argtypes = [vp]
-    lib.nmp_pipe_destroy.restype = None
     lib.nmp_type_size.argtypes = [C.c_int]
     lib.nmp_type_size.restype = C.c_int64
     lib.nmp_frh2o.argtypes = [vp, C.c_int64, vp, vp, vp, vp, vp, vp, vp]
@@ -138,11 +130,11 @@ def load(build_if_missing: bool = False):
     return lib
 
 
-EXPORTED_SYMBOLS = ["nmp_read_tables", "nmp_init", "nmp_step", "nmp_step_binned", "nmp_rebin", "nmp_forcing_synth",
+EXPORTED_SYMBOLS = ["nmp_read_tables", "nmp_init", "nmp_step", "nmp_step_binned", "nmp_rebin", "nmp_forcing_synth", "nmp_forcing_from_ldasin",
                     "nmp_run", "nmp_run_out", "nmp_frh2o", "nmp_frh2o_host", "nmp_calhum",
                     "nmp_calhum_host",
                     "nmp_state_from_aos", "nmp_sflx_columns", "nmp_sflx_column",
-                    "nmp_engine_info", "nmp_option_set", "nmp_set_launch_variant", "nmp_set_vege_cap", "nmp_pipe_create", "nmp_pipe_step", "nmp_pipe_join", "nmp_pipe_stream", "nmp_pipe_destroy", "nmp_type_size", "nmp_set_math", "nmp_set_cols_per_wave", "nmp_finalize", "nmp_strerror",
+                    "nmp_engine_info", "nmp_option_set", "nmp_set_launch_variant", "nmp_type_size", "nmp_set_math", "nmp_set_cols_per_wave", "nmp_finalize", "nmp_strerror",
                     "nmp_abi_version", "nmp_build_hash"]
 
 

@@ -239,9 +239,10 @@ def read_state(path: str, grid: Grid, dtype=np.float32):
 
 # ---- LDASIN ---------------------------------------------------------------------
 def write_ldasin(path: str, grid: Grid, forcing: np.ndarray, t: datetime.datetime,
-                 extras: bool = True):
-    """One LDASIN file from a (12, n) forcing slice; `extras` also stores COSZ,
-    CO2AIR and O2AIR so the file reproduces the slice exactly."""
+                 extras=True):
+    """One LDASIN file from a (12, n) forcing slice; `extras` (True, or a
+    tuple of some of "COSZ", "CO2AIR", "O2AIR") also stores those fields, so
+    that with all three the file reproduces the slice exactly."""
     ny, nx = grid.shape
     f = netcdf_file(path, "w")
     try:
@@ -252,8 +253,8 @@ def write_ldasin(path: str, grid: Grid, forcing: np.ndarray, t: datetime.datetim
         dims = ("Time", "south_north", "west_east")
         names = dict(LDASIN_MAP)
         names.pop("SFCPRS")  # SFCPRS and PSFC share the PSFC variable
-        if extras:
-            names.update(COSZ="COSZ", CO2AIR="CO2AIR", O2AIR="O2AIR")
+        for x in (("COSZ", "CO2AIR", "O2AIR") if extras is True else (extras or ())):
+            names[x] = x
         for fld, var in names.items():
             v = f.createVariable(var, "f4", dims)
             v[0] = grid.scatter(forcing[L.FORCING.index(fld)].astype(np.float32))
@@ -274,38 +275,101 @@ def read_ldasin(path: str) -> dict:
 class LdasinForcing:
     """Forcing provider for driver.OfflineDriver from LDASIN files: the file of
     the latest input time <= the step's start time (input_frequency, counted
-    from the run's start), held constant over the input interval."""
+    from the run's start), held constant over the input interval.
+
+    Two forms: `__call__` gives the 12 noahmp_sflx forcing fields built on the
+    host; `raw` gives the LDASIN block as the files carry it (the 8 variables
+    plus the step's COSZ, fp32, layout.LDASIN order), from which the engine
+    forms the other fields on the device (nmp_forcing_from_ldasin) -- a third
+    fewer bytes to build and upload per step, the same values.
+
+    Both are filled by `threads` host threads over column chunks (numpy
+    releases the GIL in its elementwise loops); every element is computed by
+    the same expression as in one pass, so the values do not depend on it.
+    COSZ, a double cosine per column and step, dominated the host's time."""
 
     def __init__(self, indir: str, grid: Grid, begin: datetime.datetime,
-                 every: datetime.timedelta, cols: slice | None = None):
+                 every: datetime.timedelta, cols: slice | None = None, threads: int | None = None):
         """cols: the land points this rank steps, in engine order (a slice or an
-        index array; default: all of them in grid order)."""
+        index array; default: all of them in grid order).  threads: host
+        threads (default NMP_HOST_THREADS, else 8)."""
         self.indir, self.grid, self.begin, self.every = indir, grid, begin, every
         self.cols = cols if cols is not None else slice(0, grid.n)
         self._t, self._fields = None, None
+        self.lat, self.lon = self.grid.lat_rad[self.cols], self.grid.lon_rad[self.cols]
+        # the latitude factors of COSZ, once (timeman.cosz evaluates the same
+        # numpy functions on the same values every step)
+        self._sincos_lat = (np.sin(self.lat), np.cos(self.lat))
+        self.threads = max(1, int(threads if threads is not None else
+                                  os.environ.get("NMP_HOST_THREADS", 8)))
+        self._pool = None
 
     def input_time(self, t: datetime.datetime) -> datetime.datetime:
         k = (t - self.begin) // self.every
         return self.begin + k * self.every
 
-    def __call__(self, step: int, t: datetime.datetime) -> np.ndarray:
+    def fields(self, t: datetime.datetime) -> dict:
+        """The LDASIN variables of the step starting at t (this rank's columns)."""
         ti = self.input_time(t)
         if ti != self._t:
             raw = read_ldasin(ldasin_path(self.indir, ti))
             self._fields = {k: self.grid.columns(v)[self.cols] for k, v in raw.items()}
             self._t = ti
-        fl = self._fields
-        lat, lon = self.grid.lat_rad[self.cols], self.grid.lon_rad[self.cols]
-        n = lat.shape[0]
-        f = np.empty((L.NFORCING, n), np.float32)
-        for fld, var in LDASIN_MAP.items():
-            f[L.FORCING.index(fld)] = fl[var]
-        psfc = fl["PSFC"].astype(np.float64)
-        f[L.FORCING.index("COSZ")] = fl["COSZ"] if "COSZ" in fl else timeman.cosz(
-            lat, lon, timeman.julian(t), timeman.yearlen(t.year))
-        f[L.FORCING.index("CO2AIR")] = fl["CO2AIR"] if "CO2AIR" in fl else 395.0e-6 * psfc
-        f[L.FORCING.index("O2AIR")] = fl["O2AIR"] if "O2AIR" in fl else 0.209 * psfc
+        return self._fields
+
+    def _chunks(self, fill):
+        """fill(slice) over column chunks, on the provider's threads."""
+        n = self.lat.shape[0]
+        k = min(self.threads, max(1, n // 65536))
+        sl = [slice(n * i // k, n * (i + 1) // k) for i in range(k)]
+        if k == 1:
+            fill(sl[0])
+            return
+        if self._pool is None:
+            from concurrent.futures import ThreadPoolExecutor
+            self._pool = ThreadPoolExecutor(self.threads)
+        for fut in [self._pool.submit(fill, c) for c in sl]:
+            fut.result()
+
+    def _cosz(self, fl: dict, t: datetime.datetime, c: slice) -> np.ndarray:
+        if "COSZ" in fl:
+            return fl["COSZ"][c]
+        return timeman.cosz(self.lat[c], self.lon[c], timeman.julian(t), timeman.yearlen(t.year),
+                            sincos_lat=(self._sincos_lat[0][c], self._sincos_lat[1][c]))
+
+    def __call__(self, step: int, t: datetime.datetime, out: np.ndarray | None = None):
+        fl = self.fields(t)
+        f = np.empty((L.NFORCING, self.lat.shape[0]), np.float32) if out is None else out
+        F = L.FORCING.index
+
+        def fill(c):
+            for fld, var in LDASIN_MAP.items():
+                f[F(fld), c] = fl[var][c]
+            # every field is an fp32 value (the LDASIN precision), also when
+            # `out` is an fp64 engine's buffer
+            psfc = fl["PSFC"][c].astype(np.float64)
+            f32 = np.float32
+            f[F("COSZ"), c] = np.asarray(self._cosz(fl, t, c)).astype(f32)
+            f[F("CO2AIR"), c] = fl["CO2AIR"][c] if "CO2AIR" in fl else (395.0e-6 * psfc).astype(f32)
+            f[F("O2AIR"), c] = fl["O2AIR"][c] if "O2AIR" in fl else (0.209 * psfc).astype(f32)
+        self._chunks(fill)
         return f
+
+    def raw(self, step: int, t: datetime.datetime, out: np.ndarray | None = None):
+        """(NLDASIN, n) fp32 LDASIN block of the step starting at t, written
+        into `out` when given (e.g. a pinned upload buffer); None when the file
+        carries CO2AIR / O2AIR of its own (then only the 12-field form holds
+        them)."""
+        fl = self.fields(t)
+        if "CO2AIR" in fl or "O2AIR" in fl:
+            return None
+        r = np.empty((L.NLDASIN, self.lat.shape[0]), np.float32) if out is None else out
+
+        def fill(c):
+            for i, var in enumerate(L.LDASIN):
+                r[i, c] = self._cosz(fl, t, c) if var == "COSZ" else fl[var][c]
+        self._chunks(fill)
+        return r
 
 
 # ---- LDASOUT ----------------------------------------------------------------------

@@ -30,10 +30,14 @@ def step_times(begin: _dt.datetime, end: _dt.datetime, dt_seconds: float):
     return [begin + _dt.timedelta(seconds=dt_seconds * (i + 1)) for i in range(n)]
 
 
-def cosz(lat_rad, lon_rad, jul: float, ylen: int):
-    """Cosine of the solar zenith angle (simple declination + hour angle)."""
+def cosz(lat_rad, lon_rad, jul: float, ylen: int, sincos_lat=None):
+    """Cosine of the solar zenith angle (simple declination + hour angle).
+    sincos_lat: (np.sin(lat), np.cos(lat)) precomputed by a caller that
+    evaluates many steps of the same columns (the same values)."""
     decl = 0.409 * math.sin(2.0 * math.pi * (jul - 80.0) / ylen)
     hour_utc = (jul - math.floor(jul)) * 24.0
     ha = 2.0 * math.pi * (hour_utc / 24.0) + np.asarray(lon_rad) - math.pi
-    lat = np.asarray(lat_rad)
-    return np.sin(lat) * math.sin(decl) + np.cos(lat) * math.cos(decl) * np.cos(ha)
+    if sincos_lat is None:
+        lat = np.asarray(lat_rad)
+        sincos_lat = (np.sin(lat), np.cos(lat))
+    return sincos_lat[0] * math.sin(decl) + sincos_lat[1] * math.cos(decl) * np.cos(ha)

@@ -8,8 +8,7 @@ and bare Newton loops, after the fast loop has changed TV/TAH/EAH, QSFC and
 the first iteration's stomata outputs.  Those lanes re-run the loop with IEEE
 division from restored inputs (sflx_kernel.hip vege_loop / bare_loop).  Every
 column must still equal the C restatement of the reference bit for bit, in
-both occupancy instantiations (the full one also with the loop capped at 6
-iterations and resumed) and at diagnostics levels NONE and FULL, and
+both occupancy instantiations and at diagnostics levels NONE and FULL, and
 the device counter must show the in-loop windows fired.
 
     NOAHMP_ENGINE_LIB=.../lib_probe_midloop.so python tests/probe_midloop.py
@@ -57,14 +56,10 @@ def main():
         f = cases.forcing_step(cols, jul, yl, 0, seed=seed)
         est, eisn, edg, _ = port.step(load_params(), tuple(opts), cases.CASE_NML_ZSOIL, dt, yl,
                                       jul, cols.state, cols.isnow, cols.static_f, cols.static_i, f)
-        for variant in ("small", "full", "full_cap6"):
+        for variant in ("small", "full"):
             for level in ("none", "full"):
                 eng = Engine(P, L.CASE_NML_OPTIONS, device=0)
-                base, _, cap = variant.partition("_cap")
-                assert eng.launch_variant(base) == base
-                # capped: lanes resumed from their saved context may still
-                # leave the window later and re-run from the step's inputs
-                eng.vege_cap(int(cap) if cap else 0)
+                assert eng.launch_variant(variant) == variant
                 cs = ColumnState.from_host(cols, "cuda:0")
                 raw.nmp_debug_fallback_count(1, None)
                 if level == "full":

@@ -65,6 +65,9 @@ def test_layout_matches_header():
         assert e[f"NMP_I_{n}"] == i
     for i, n in enumerate(L.FORCING):
         assert e[f"NMP_A_{n}"] == i
+    for i, n in enumerate(L.LDASIN):
+        assert e[f"NMP_L_{n}"] == i
+    assert e["NMP_NLDASIN"] == L.NLDASIN
     for i, n in enumerate(L.DIAG_FULL):
         assert e[f"NMP_D_{n}"] == i
     for i, n in enumerate(L.DIAG_OUT):
@@ -82,7 +85,7 @@ def test_params_struct_size():
 
 
 def test_abi_version_and_errors(engine_lib):
-    assert engine_lib.nmp_abi_version() == 6
+    assert engine_lib.nmp_abi_version() == 7
     for code in (0, -1, -2, -3, -4, -5, -6, -99):
         assert engine_lib.nmp_strerror(code)
     assert b"year boundary" in engine_lib.nmp_strerror(-6)

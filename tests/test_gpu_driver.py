@@ -59,9 +59,14 @@ def test_restart_round_trip(engine_lib, tmp_path):
     assert bit_equal(b.cs.state.cpu().numpy(), g["states"][-1]).all()
 
 
-def test_driver_from_netcdf_files(engine_lib, tmp_path):
+@pytest.mark.parametrize("extras,device_fields", [(True, False), (("COSZ",), True),
+                                                   (("COSZ",), False)])
+def test_driver_from_netcdf_files(engine_lib, tmp_path, extras, device_fields):
     """namelist -> static / init / LDASIN netCDF files (ncio.py) -> time loop ->
-    LDASOUT netCDF and a netCDF restart: the reference trajectory bit for bit."""
+    LDASOUT netCDF and a netCDF restart: the reference trajectory bit for bit.
+    Files without CO2AIR / O2AIR go up as the LDASIN block and the engine forms
+    the 12 forcing fields (nmp_forcing_from_ldasin); files carrying them, or
+    ldasin_upload=False, go up as the 12-field host form."""
     from noahmp_amd import ncio
     from test_config import write_case
     from test_ncio import grid_for
@@ -79,11 +84,17 @@ def test_driver_from_netcdf_files(engine_lib, tmp_path):
     ncio.write_static(str(static), cols, grid)
     ncio.write_state(str(init), grid, g["state0"], g["isnow0"], cfg.begdatetime)
     for k, t in enumerate([cfg.begdatetime + i * cfg.timestep for i in range(96)]):
-        ncio.write_ldasin(ncio.ldasin_path(str(indir), t), grid, g["forcing"][k], t)
-    drv = driver.OfflineDriver.from_files(cfg)
+        ncio.write_ldasin(ncio.ldasin_path(str(indir), t), grid, g["forcing"][k], t,
+                          extras=extras)
+    kw = dict(ldasin_upload=device_fields)
+    drv = driver.OfflineDriver.from_files(cfg, **kw)
     assert np.array_equal(np.sort(drv.perm), np.arange(32))  # the coherent column order
     drv.run()
     assert drv.step_index == 96
+    # which upload ran: the LDASIN block, or the 12 fields
+    raw_path = extras is not True and device_fields
+    assert (drv.raw_upload is not None and drv.raw_upload.count == 96) == raw_path
+    assert drv.upload.count == (0 if raw_path else 96)
     assert bit_equal(drv.to_grid_order(drv.cs.state.cpu().numpy()), g["states"][-1]).all()
     files = sorted(glob.glob(os.path.join(cfg.outdir, "*.LDASOUT_DOMAIN1")))
     assert len(files) == 8
@@ -92,15 +103,15 @@ def test_driver_from_netcdf_files(engine_lib, tmp_path):
         if name != "T2M":
             assert bit_equal(d[i], g["diags"][-1][L.DIAG_FULL.index(name)]).all(), name
     # netCDF restart half way, resumed by a fresh driver
-    a = driver.OfflineDriver.from_files(cfg, write=False).run(nsteps=40)
+    a = driver.OfflineDriver.from_files(cfg, write=False, **kw).run(nsteps=40)
     path = str(tmp_path / "RESTART.nc")
     a.save_restart(path)
-    b = driver.OfflineDriver.from_files(cfg, init=path, write=False)
+    b = driver.OfflineDriver.from_files(cfg, init=path, write=False, **kw)
     assert b.step_index == 40
     b.run()
     assert bit_equal(b.to_grid_order(b.cs.state.cpu().numpy()), g["states"][-1]).all()
     # grid order (order=None) gives the same bits
-    c = driver.OfflineDriver.from_files(cfg, init=path, write=False, order=None).run()
+    c = driver.OfflineDriver.from_files(cfg, init=path, write=False, order=None, **kw).run()
     assert bit_equal(c.cs.state.cpu().numpy(), g["states"][-1]).all()
 
 

@@ -71,3 +71,47 @@ def test_device_forcing_is_stateless_over_ranges(engine_lib):
     torch.cuda.synchronize()
     assert torch.equal(a.view(torch.int32), b.view(torch.int32))
     eng.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("precision", [4, 8])
+def test_forcing_from_ldasin_equals_host_reader(engine_lib, precision):
+    """nmp_forcing_from_ldasin: the 12 forcing fields the engine forms from the
+    uploaded LDASIN block (8 file variables + COSZ, fp32) are, bit for bit,
+    the fields the host reader builds (ncio.LdasinForcing.__call__: SFCPRS =
+    PSFC, CO2AIR / O2AIR = 395e-6 / 0.209 PSFC in double rounded to fp32), then
+    widened to the engine precision; column ranges give the one-launch result."""
+    from noahmp_amd import ncio
+    from noahmp_amd.engine import Engine
+    from noahmp_amd.params import Params
+    dt = torch.float32 if precision == 4 else torch.float64
+    n = 70_001
+    cols = cases.make_columns(n, "conus", Params.builtin().as_dict(), seed=6, julian=100.0)
+    f = cases.forcing_step(cols, 100.25, 366, 3, seed=6)
+    # pressures the fp32 file holds (a double product of an fp32 pressure
+    # rounds differently from one of the generator's double pressure)
+    fl = {var: f[L.FORCING.index(fld)] for fld, var in ncio.LDASIN_MAP.items()}
+    fl["COSZ"] = f[L.FORCING.index("COSZ")]
+    raw = np.stack([fl[v] for v in L.LDASIN]).astype(np.float32)
+    want = np.empty((L.NFORCING, n), np.float32)
+    for fld, var in ncio.LDASIN_MAP.items():
+        want[L.FORCING.index(fld)] = fl[var]
+    want[L.FORCING.index("COSZ")] = fl["COSZ"]
+    psfc = fl["PSFC"].astype(np.float64)
+    want[L.FORCING.index("CO2AIR")] = 395.0e-6 * psfc
+    want[L.FORCING.index("O2AIR")] = 0.209 * psfc
+    want = want.astype(np.float32 if precision == 4 else np.float64)
+    eng = Engine(Params.builtin(), L.CASE_NML_OPTIONS, device=0, precision=precision)
+    r = torch.as_tensor(raw, device=DEV)
+    a = torch.zeros((L.NFORCING, n), dtype=dt, device=DEV)
+    b = torch.full_like(a, float("nan"))
+    eng.forcing_from_ldasin(r, a)
+    for lo, hi in ((0, 4_097), (4_097, 50_000), (50_000, n)):
+        eng.forcing_from_ldasin(r, b, cols=(lo, hi))
+    torch.cuda.synchronize()
+    iv = torch.int32 if precision == 4 else torch.int64
+    got = a.cpu().numpy()
+    assert np.array_equal(got.view(np.int32 if precision == 4 else np.int64),
+                          want.view(np.int32 if precision == 4 else np.int64))
+    assert torch.equal(a.view(iv), b.view(iv))
+    eng.close()

@@ -40,11 +40,7 @@ DEV = "cuda:0"
 # launch runs.  Register allocation differs between them, so each is pinned
 # to the reference on its own ("What's weak" 1).
 VARIANTS = ["small", "full"]
-# fp32 bit-exact tests also run the full kernel with the canopy Newton loop
-# capped at 6 iterations (nmp_set_vege_cap): most vegetated lanes then leave
-# the main launch and finish in the resume launch from their saved context
-# (DESIGN.md "Cap and resume")
-VARIANTS32 = VARIANTS + ["full_cap6"]
+VARIANTS32 = VARIANTS
 
 
 @pytest.fixture(scope="module")
@@ -60,9 +56,7 @@ def engines(engine_lib):
                 tables[tags] = Params.builtin(*tags)
             cache[key] = Engine(tables[tags], dict(zip(L.OPTION_NAMES, key[0])), device=0,
                                 precision=precision, math=math)
-            base, _, cap = variant.partition("_cap")
-            assert cache[key].launch_variant(base) == base
-            assert cache[key].vege_cap(int(cap) if cap else 0) == (int(cap) if cap else 0)
+            assert cache[key].launch_variant(variant) == variant
         return cache[key]
     return get
 
@@ -1115,106 +1109,3 @@ def test_midloop_domain_exit_bit_exact():
     for run in res["runs"]:
         print(run)
     assert r.returncode == 0 and res["ok"], res
-
-
-@pytest.mark.parametrize("opt_veg", [1, 2])
-def test_vege_cap_resume_bit_exact_for_every_cap(engines, oracle_port, opt_veg):
-    """Cap and resume (nmp_set_vege_cap): the canopy Newton loop of
-    the full fp32 kernel stopped after K iterations for K = 2 (every lane that
-    reaches iteration 3 resumes), 3, 5, 10, 15 and 19 (only the last
-    iteration resumes), the capped columns finished by the resume launch.
-    8,192 mixed columns at diagnostics level FULL, both compiled option sets
-    (opt_veg 1 and 2): every column equals the C restatement bit for bit --
-    state, ISNOW, all 58 outputs -- and the run without a cap."""
-    from noahmp_amd.engine import ColumnState
-    P = __import__("noahmp_amd.params", fromlist=["Params"]).Params.builtin()
-    opts = tuple(dict(L.CASE_NML_OPTIONS, opt_veg=opt_veg)[k] for k in L.OPTION_NAMES)
-    n = 8192
-    cols = cases.make_columns(n, "mixed", P.as_dict(), seed=77, julian=180.0)
-    f = cases.forcing_step(cols, 180.3, 366, 0, seed=77)
-    est, eisn, edg, _ = oracle_port.step(load_params(), opts, cases.CASE_NML_ZSOIL, 1800.0, 366,
-                                         180.3, cols.state, cols.isnow, cols.static_f,
-                                         cols.static_i, f)
-    for k in (0, 2, 3, 5, 10, 15, 19):
-        eng = engines(opts, variant=f"full_cap{k}" if k else "full")
-        assert eng.vege_cap() == k
-        cs = ColumnState.from_host(cols, DEV)
-        diag = torch.zeros((L.NDIAG_FULL, n), device=DEV)
-        eng.step(cs, torch.as_tensor(f, device=DEV), cases.CASE_NML_ZSOIL, 1800.0, 180.3, 366,
-                 diag, L.DIAG_FULL_LEVEL)
-        torch.cuda.synchronize()
-        ok = bit_equal(cs.state.cpu().numpy(), est).all(0) & \
-            bit_equal(diag.cpu().numpy(), edg).all(0) & (cs.isnow.cpu().numpy() == eisn)
-        assert ok.all(), f"cap {k}: {(~ok).sum()} of {n} columns differ"
-
-
-def test_vege_cap_stream_ranges_equal_plain(engines):
-    """Cap and resume under the bench's two concurrent stream ranges
-    (StreamShards): each stream has its own side buffer.  24 steps of 65,536
-    + 999 mixed columns with output every 3rd step: state and every output
-    step equal the uncapped run bit for bit."""
-    from noahmp_amd.engine import ColumnState, StreamShards
-    P = __import__("noahmp_amd.params", fromlist=["Params"]).Params.builtin()
-    opts = tuple(L.CASE_NML_OPTIONS[k] for k in L.OPTION_NAMES)
-    n = 65536 + 999
-    cols = cases.make_columns(n, "mixed", P.as_dict(), seed=78, julian=180.0)
-    F = [torch.as_tensor(cases.forcing_step(cols, 180.0 + s / 48.0, 366, s, seed=78), device=DEV)
-         for s in range(24)]
-
-    def run(variant):
-        eng = engines(opts, variant=variant)
-        cs = ColumnState.from_host(cols, DEV)
-        sh = StreamShards(eng, cs, 2)
-        outs = []
-        for s in range(24):
-            d = torch.zeros((L.NDIAG_OUT, n), device=DEV) if s % 3 == 2 else None
-            sh.step(F[s], cases.CASE_NML_ZSOIL, 1800.0, 180.0 + s / 48.0, 366, d,
-                    L.DIAG_OUT_LEVEL if d is not None else L.DIAG_NONE)
-            if d is not None:
-                outs.append(d)
-        sh.join()
-        torch.cuda.synchronize()
-        return cs.state.cpu().numpy(), cs.isnow.cpu().numpy(), [o.cpu().numpy() for o in outs]
-
-    st0, isn0, out0 = run("full")
-    st1, isn1, out1 = run("full_cap8")
-    assert bit_equal(st1, st0).all() and np.array_equal(isn1, isn0)
-    for a, b in zip(out1, out0):
-        assert bit_equal(a, b).all()
-
-
-@pytest.mark.parametrize("k", [2, 10])
-def test_vege_cap_pipeline_steps_bit_exact(engines, k):
-    """The deferred cap-and-resume pipeline (nmp_pipe_*, Engine.pipe): the
-    columns capped at step t finish on the companion stream, and take step t+1
-    there too while the caller's stream runs step t+1 of the others.  One
-    pipeline over 65,536 + 77 mixed columns, 8 steps with all 58 outputs
-    every step, the canopy loop capped at k (2: nearly every vegetated lane
-    goes through the companion; 10: the stragglers): after each step's join,
-    state, ISNOW, status and outputs equal the uncapped engine's bit for bit."""
-    from noahmp_amd.engine import ColumnState
-    P = __import__("noahmp_amd.params", fromlist=["Params"]).Params.builtin()
-    opts = tuple(L.CASE_NML_OPTIONS[kk] for kk in L.OPTION_NAMES)
-    n = 65536 + 77
-    cols = cases.make_columns(n, "mixed", P.as_dict(), seed=79, julian=180.0)
-    F = [torch.as_tensor(cases.forcing_step(cols, 180.0 + s / 48.0, 366, s, seed=79), device=DEV)
-         for s in range(8)]
-    ref_eng = engines(opts, variant="full")
-    eng = engines(opts, variant=f"full_cap{k}")
-    a, b = ColumnState.from_host(cols, DEV), ColumnState.from_host(cols, DEV)
-    pipe = eng.pipe(b)
-    for s in range(8):
-        da = torch.zeros((L.NDIAG_FULL, n), device=DEV)
-        db = torch.zeros((L.NDIAG_FULL, n), device=DEV)
-        ref_eng.step(a, F[s], cases.CASE_NML_ZSOIL, 1800.0, 180.0 + s / 48.0, 366, da,
-                     L.DIAG_FULL_LEVEL)
-        pipe.step(F[s], cases.CASE_NML_ZSOIL, 1800.0, 180.0 + s / 48.0, 366, db,
-                  L.DIAG_FULL_LEVEL)
-        pipe.join()
-        torch.cuda.synchronize()
-        ok = bit_equal(b.state.cpu().numpy(), a.state.cpu().numpy()).all(0) & \
-            bit_equal(db.cpu().numpy(), da.cpu().numpy()).all(0) & \
-            (b.isnow.cpu().numpy() == a.isnow.cpu().numpy()) & \
-            (b.status.cpu().numpy() == a.status.cpu().numpy())
-        assert ok.all(), f"cap {k}, step {s}: {(~ok).sum()} of {n} columns differ"
-    pipe.close()

@@ -82,6 +82,22 @@ def test_ldasin_round_trip_and_derived_fields(tmp_path, ref_params):
     psfc = f[L.FORCING.index("PSFC")].astype(np.float64)
     assert np.array_equal(bits(g[L.FORCING.index("CO2AIR")]), bits(np.float32(395e-6 * psfc)))
     assert np.array_equal(g[L.FORCING.index("SFCPRS")], f[L.FORCING.index("PSFC")])
+    # the LDASIN block the engine expands on the device (nmp_forcing_from_ldasin):
+    # the file's variables + the same COSZ; restated here as the kernel forms
+    # the fields, it gives the host reader's 12 bit for bit
+    prov2 = ncio.LdasinForcing(str(d), grid, T0, datetime.timedelta(hours=1))
+    raw = prov2.raw(2, t)
+    assert raw.dtype == np.float32 and raw.shape == (L.NLDASIN, 32)
+    R = {v: raw[i] for i, v in enumerate(L.LDASIN)}
+    x = {"SFCTMP": R["T2D"], "SFCPRS": R["PSFC"], "PSFC": R["PSFC"], "UU": R["U2D"],
+         "VV": R["V2D"], "Q2": R["Q2D"], "SOLDN": R["SWDOWN"], "LWDN": R["LWDOWN"],
+         "PRCP": R["RAINRATE"], "COSZ": R["COSZ"],
+         "CO2AIR": np.float32(395.0e-6 * R["PSFC"].astype(np.float64)),
+         "O2AIR": np.float32(0.209 * R["PSFC"].astype(np.float64))}
+    assert np.array_equal(bits(np.stack([x[k] for k in L.FORCING])), bits(g))
+    # a file with its own CO2AIR / O2AIR has no block form
+    ncio.write_ldasin(ncio.ldasin_path(str(d), T0), grid, f, T0, extras=("CO2AIR",))
+    assert ncio.LdasinForcing(str(d), grid, T0, datetime.timedelta(hours=1)).raw(0, T0) is None
     with pytest.raises(FileNotFoundError):
         prov(8, T0 + datetime.timedelta(hours=2))
 

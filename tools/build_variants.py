@@ -186,10 +186,6 @@ VARIANTS = {
     # back on ("drop": flag pairs removed from build.FLAGS)
     "licm": {"drop": [("-mllvm", "-disable-machine-licm")]},
     "pre": {"drop": [("-mllvm", "-enable-pre=false")]},
-    "cap8": {"f32": ["-DNMP_VEGE_CAP_PROBE=8"]},
-    "cap10": {"f32": ["-DNMP_VEGE_CAP_PROBE=10"]},
-    "cap12": {"f32": ["-DNMP_VEGE_CAP_PROBE=12"]},
-    "cap14": {"f32": ["-DNMP_VEGE_CAP_PROBE=14"]},
 }
 if __name__ == "__main__":
     names = sys.argv[1:] or list(VARIANTS)
