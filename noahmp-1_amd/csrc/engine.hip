@@ -141,6 +141,11 @@ void fill_args(nmp::KArgs<T>& a, const nmp_engine* e, int64_t ncol, int64_t ld,
   a.cost = cost;
   a.ficeold = static_cast<const T*>(ficeold);
   a.cpw = cols_per_wave(e, ncol);
+#ifdef NMP_TRUNC_RUNTIME
+  // (probe builds) env NMP_TRUNC_AT: the phase mark the step returns at
+  static const int trunc_at = std::getenv("NMP_TRUNC_AT") ? std::atoi(std::getenv("NMP_TRUNC_AT")) : 99;
+  a.trunc_at = trunc_at;
+#endif
 }
 
 int launch(nmp_engine* e, int64_t ncol, int64_t ld, const float zsoil[4], float dt,

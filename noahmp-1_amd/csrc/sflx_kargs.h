@@ -47,6 +47,9 @@ struct KArgs {
   // columns stepped per 64-lane wave (8..64, a multiple of 8): below 64 the
   // launch spreads a small column set over more waves (small-N latency hiding)
   int cpw;
+#ifdef NMP_TRUNC_RUNTIME
+  int trunc_at;  // (probe builds) phase mark the step returns at (sflx_kernel.hip)
+#endif
 };
 
 template <class T, bool R>

@@ -985,9 +985,22 @@ struct PhaseClock {
     ph = next;
   }
 };
-#define NMP_PHASE(i) pclk.mark(i)
+#define NMP_PHASE_MARK(i) pclk.mark(i)
 #else
-#define NMP_PHASE(i) ((void)0)
+#define NMP_PHASE_MARK(i) ((void)0)
+#endif
+// Optional per-phase truncation (build with -DNMP_TRUNC_RUNTIME; tools only,
+// tools/phase_counters.sh): the column's step returns at phase mark
+// A.trunc_at (a kernel argument, so nothing before the mark is optimised
+// away); consecutive marks' counters differ by one phase.
+#ifdef NMP_TRUNC_RUNTIME
+#define NMP_PHASE(i)                   \
+  do {                                 \
+    NMP_PHASE_MARK(i);                 \
+    if (A.trunc_at == (i)) return;     \
+  } while (0)
+#else
+#define NMP_PHASE(i) NMP_PHASE_MARK(i)
 #endif
 
 // Optional per-wave timing (build with -DNMP_WAVE_TIMING; tools only): each

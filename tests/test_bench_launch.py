@@ -28,7 +28,7 @@ def run(args, timeout=180, **env):
     return p.returncode, lines, p.stderr
 
 
-@pytest.mark.parametrize("n", [2, 3])
+@pytest.mark.parametrize("n", [2, 3, 8])
 def test_spawned_ranks_report_world(n):
     rc, lines, err = run(["--gpus", str(n), "--launch-probe", "--ncol", "500"])
     assert rc == 0, err[-2000:]
@@ -36,6 +36,28 @@ def test_spawned_ranks_report_world(n):
     ln = lines[0]
     assert ln["n_gpus"] == n and ln["ranks_joined"] == n
     assert ln["ncol_total"] == n * 500 and ln["first_col_sum"] == 500 * n * (n - 1) // 2
+
+
+def test_torchrun_eight_ranks_report_world():
+    """The driver's own N = 8 launch line (torch.distributed.run, one process
+    per rank, rendezvous on 127.0.0.1) with --launch-probe: eight ranks join,
+    rank 0 alone prints one line with n_gpus 8 and every rank's block."""
+    import socket
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    e = {k: v for k, v in os.environ.items()
+         if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    p = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+                        "--nproc-per-node", "8", "--master-addr", "127.0.0.1", "--master-port",
+                        str(port), BENCH, "--gpus", "8", "--launch-probe", "--ncol", "300"],
+                       capture_output=True, text=True, timeout=300, env=e)
+    assert p.returncode == 0, p.stderr[-2000:]
+    lines = [json.loads(x) for x in p.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1, lines
+    ln = lines[0]
+    assert ln["n_gpus"] == 8 and ln["ranks_joined"] == 8
+    assert ln["ncol_total"] == 8 * 300 and ln["first_col_sum"] == 300 * 8 * 7 // 2
 
 
 def test_failed_rank_fails_the_job():

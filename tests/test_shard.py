@@ -1,4 +1,4 @@
-"""Multi-rank path on CPU (gloo, world sizes 2 and 3, ragged shards): column
+"""Multi-rank path on CPU (gloo, world sizes 2, 3 and 8, ragged shards): column
 sharding + the output-step diagnostics gather reproduce the single-rank
 result bit for bit (SURVEY.md 8e correctness test).  Per-shard physics is
 computed by the oracle restatement (this is a test of the sharding plumbing)."""
@@ -89,9 +89,11 @@ def _worker(rank, world, port, out_path, ncol, dst=None):
 
 
 @pytest.mark.parametrize("world,ncol,dst", [(2, 2048, 0), (2, 2047, None), (3, 2048, 0),
-                                            (3, 2047, 2), (3, 2045, None)],
+                                            (3, 2047, 2), (3, 2045, None), (8, 2045, None),
+                                            (8, 2043, 5)],
                          ids=["w2-even-root", "w2-ragged-all", "w3-ragged-root",
-                              "w3-ragged-to-2", "w3-ragged-all"])
+                              "w3-ragged-to-2", "w3-ragged-all", "w8-ragged-all",
+                              "w8-ragged-to-5"])
 def test_gloo_output_loop_equals_single_rank(oracle_port, tmp_path, world, ncol, dst):
     """SURVEY 8e correctness test of the bench/driver output loop: ragged shards
     (shard_range), double-buffered asynchronous gathers with buffer reuse, to
