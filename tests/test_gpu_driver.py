@@ -59,14 +59,11 @@ def test_restart_round_trip(engine_lib, tmp_path):
     assert bit_equal(b.cs.state.cpu().numpy(), g["states"][-1]).all()
 
 
-@pytest.mark.parametrize("extras,device_fields", [(True, False), (("COSZ",), True),
-                                                   (("COSZ",), False)])
-def test_driver_from_netcdf_files(engine_lib, tmp_path, extras, device_fields):
+def test_driver_from_netcdf_files(engine_lib, tmp_path):
     """namelist -> static / init / LDASIN netCDF files (ncio.py) -> time loop ->
     LDASOUT netCDF and a netCDF restart: the reference trajectory bit for bit.
-    Files without CO2AIR / O2AIR go up as the LDASIN block and the engine forms
-    the 12 forcing fields (nmp_forcing_from_ldasin); files carrying them, or
-    ldasin_upload=False, go up as the 12-field host form."""
+    The files carry the trajectory's own CO2AIR / O2AIR, so the driver uploads
+    the 12-field host form."""
     from noahmp_amd import ncio
     from test_config import write_case
     from test_ncio import grid_for
@@ -84,17 +81,11 @@ def test_driver_from_netcdf_files(engine_lib, tmp_path, extras, device_fields):
     ncio.write_static(str(static), cols, grid)
     ncio.write_state(str(init), grid, g["state0"], g["isnow0"], cfg.begdatetime)
     for k, t in enumerate([cfg.begdatetime + i * cfg.timestep for i in range(96)]):
-        ncio.write_ldasin(ncio.ldasin_path(str(indir), t), grid, g["forcing"][k], t,
-                          extras=extras)
-    kw = dict(ldasin_upload=device_fields)
-    drv = driver.OfflineDriver.from_files(cfg, **kw)
+        ncio.write_ldasin(ncio.ldasin_path(str(indir), t), grid, g["forcing"][k], t)
+    drv = driver.OfflineDriver.from_files(cfg)
     assert np.array_equal(np.sort(drv.perm), np.arange(32))  # the coherent column order
     drv.run()
-    assert drv.step_index == 96
-    # which upload ran: the LDASIN block, or the 12 fields
-    raw_path = extras is not True and device_fields
-    assert (drv.raw_upload is not None and drv.raw_upload.count == 96) == raw_path
-    assert drv.upload.count == (0 if raw_path else 96)
+    assert drv.step_index == 96 and drv.upload.count == 96
     assert bit_equal(drv.to_grid_order(drv.cs.state.cpu().numpy()), g["states"][-1]).all()
     files = sorted(glob.glob(os.path.join(cfg.outdir, "*.LDASOUT_DOMAIN1")))
     assert len(files) == 8
@@ -103,16 +94,63 @@ def test_driver_from_netcdf_files(engine_lib, tmp_path, extras, device_fields):
         if name != "T2M":
             assert bit_equal(d[i], g["diags"][-1][L.DIAG_FULL.index(name)]).all(), name
     # netCDF restart half way, resumed by a fresh driver
-    a = driver.OfflineDriver.from_files(cfg, write=False, **kw).run(nsteps=40)
+    a = driver.OfflineDriver.from_files(cfg, write=False).run(nsteps=40)
     path = str(tmp_path / "RESTART.nc")
     a.save_restart(path)
-    b = driver.OfflineDriver.from_files(cfg, init=path, write=False, **kw)
+    b = driver.OfflineDriver.from_files(cfg, init=path, write=False)
     assert b.step_index == 40
     b.run()
     assert bit_equal(b.to_grid_order(b.cs.state.cpu().numpy()), g["states"][-1]).all()
     # grid order (order=None) gives the same bits
-    c = driver.OfflineDriver.from_files(cfg, init=path, write=False, order=None, **kw).run()
+    c = driver.OfflineDriver.from_files(cfg, init=path, write=False, order=None).run()
     assert bit_equal(c.cs.state.cpu().numpy(), g["states"][-1]).all()
+
+
+@pytest.mark.parametrize("precision", [4, 8])
+def test_driver_ldasin_block_equals_host_fields(engine_lib, tmp_path, precision):
+    """Standard HRLDAS files (the 8 LDASIN variables only; COSZ from the grid,
+    CO2AIR / O2AIR from PSFC): the driver uploads the LDASIN block and the
+    engine forms the 12 fields on each range's stream (nmp_forcing_from_ldasin),
+    or builds the 12 fields on the host (ldasin_upload=False).  Both runs give
+    the same state, ISNOW and LDASOUT files bit for bit, in fp32 and fp64,
+    from two host threads or one."""
+    from noahmp_amd import ncio
+    from test_config import write_case
+    from test_ncio import grid_for
+    g = load("traj_casenml.npz")
+    cols = _cols(g)
+    grid = grid_for(cols)
+    static, init, indir = tmp_path / "geo_em.d01.nc", tmp_path / "init.nc", tmp_path / "ldasin"
+    indir.mkdir()
+    nml = write_case(tmp_path)
+    text = open(nml).read().replace("'geo_em.d01.nc'", f"'{static}'").replace(
+        '"init.nc"', f'"{init}"').replace("'ldasin'", f"'{indir}'")
+    open(nml, "w").write(text)
+    cfg = config.Config(nml)
+    ncio.write_static(str(static), cols, grid)
+    ncio.write_state(str(init), grid, g["state0"], g["isnow0"], cfg.begdatetime)
+    t = cfg.begdatetime
+    for k in range(0, 96, 4):  # hourly files (input_frequency '1 hour')
+        ncio.write_ldasin(ncio.ldasin_path(str(indir), t), grid, g["forcing"][k], t, extras=False)
+        t = t + cfg.input_interval
+    runs = []
+    for ldasin, threads in ((False, 1), (True, 2)):
+        cfg.outdir = str(tmp_path / f"out_{int(ldasin)}")
+        drv = driver.OfflineDriver.from_files(cfg, precision=precision, ldasin_upload=ldasin,
+                                              host_threads=threads).run()
+        assert drv.step_index == 96
+        assert (drv.raw_upload is not None and drv.raw_upload.count == 96) == ldasin
+        assert drv.upload.count == (0 if ldasin else 96)
+        outs = [ncio.read_ldasout(f, grid) for f in sorted(
+            glob.glob(os.path.join(cfg.outdir, "*.LDASOUT_DOMAIN1")))]
+        assert len(outs) == 8
+        runs.append((drv.cs.state.cpu().numpy(), drv.cs.isnow.cpu().numpy(), outs))
+        drv.engine.close()
+    (s0, i0, o0), (s1, i1, o1) = runs
+    assert bit_equal(s1, s0).all() and np.array_equal(i1, i0)
+    for a, b in zip(o1, o0):
+        assert bit_equal(a, b).all()
+    assert np.isfinite(s1[L.s("STC")]).all()
 
 
 def test_offline_cli_runs_a_netcdf_case(engine_lib, tmp_path):

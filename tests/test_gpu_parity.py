@@ -881,6 +881,61 @@ def test_full_size_sample_vs_oracle(engines, oracle_port, kind, ncol, opt_veg, p
         assert ok.mean() >= 0.99, column_mismatch(got, st, 1e-9, 1e-9, STATE_NAMES)[1][:8]
 
 
+@pytest.mark.parametrize("rank", [0, 3])
+def test_config5_shard_bench_pipeline_vs_oracle(engines, oracle_port, rank):
+    """Config #5 as each of the 8 GPUs holds it: the
+    129,600-column shard `bench.py --kind global --ncol 129600 --precision 8
+    --opt-veg 2 --dt 3600 --out-every 1 --forcing device` steps on rank R
+    (seed 1000 + R, global columns R x 129,600 on), in the coherent order, two
+    stream ranges, forcing generated on each range's stream before its launch,
+    carbon on, the 16 output fluxes every step -- the bench's own pipeline,
+    emulated on one GPU (`--emulate-rank`).  Rank 0 is the polar band (ice
+    sheets), rank 3 the southern subtropics.  Three steps, then a seeded
+    sample of 2,048 columns through the fp64 restatement with the device's
+    forcing: |d| <= 1e-9 (1 + |x|) on >= 99 % of columns, state and fluxes."""
+    from noahmp_amd.engine import ColumnState, StreamShards
+    from noahmp_amd.order import coherent_order
+    from noahmp_amd.params import Params
+    P = Params.builtin("STAS", "USGS")
+    opts = dict(L.CASE_NML_OPTIONS, opt_veg=2)
+    eng = engines([opts[k] for k in L.OPTION_NAMES], 8)
+    n, dt, yl, seed, nsteps = 129_600, 3600.0, 366, 1000 + rank, 3
+    cols = cases.make_columns(n, "global", P.as_dict(), seed=seed, julian=180.0, first=rank * n)
+    cols = cols.take(coherent_order(cols.lon, cols.static_i, cols.isnow, "lon-snow-type",
+                                    band_deg=4.0))
+    cs = ColumnState.from_host(cols, DEV, torch.float64)
+    sh = StreamShards(eng, cs, 2)
+    clim = torch.as_tensor(cases.climate(cols), device=DEV).contiguous()
+    F = torch.empty((2, L.NFORCING, n), dtype=torch.float64, device=DEV)
+    diag = torch.zeros((L.NDIAG_OUT, n), dtype=torch.float64, device=DEV)
+    jul = [(180.0 + k * dt / 86400.0) % yl for k in range(nsteps)]
+    forc = []
+    for k in range(nsteps):
+        f = F[k % 2]
+        pre = lambda st, rng, f=f, k=k: eng.forcing_synth(  # noqa: E731
+            clim, jul[k], yl, seed, k, f, first_col=rank * n, stream=st, cols=rng)
+        sh.step(f, cases.CASE_NML_ZSOIL, dt, jul[k], yl, diag, L.DIAG_OUT_LEVEL, pre=pre)
+        sh.join()
+        torch.cuda.synchronize()
+        forc.append(f.cpu().numpy().copy())
+    idx = np.sort(np.random.default_rng(7).choice(n, 2048, replace=False))
+    idx[-1] = n - 1
+    st, isn = cols.state[:, idx], cols.isnow[idx]
+    for k in range(nsteps):
+        st, isn, dg, _ = oracle_port.step(
+            load_params(), tuple(opts[x] for x in L.OPTION_NAMES), cases.CASE_NML_ZSOIL, dt, yl,
+            float(np.float32(jul[k])), st, isn, cols.static_f[:, idx], cols.static_i[:, idx],
+            forc[k][:, idx], precision=8)
+    got = cs.state.cpu().numpy()[:, idx]
+    gd = diag.cpu().numpy()[:, idx]
+    od = np.stack([dg[L.DIAG_FULL.index(m)] for m in L.DIAG_OUT if m != "T2M"])
+    gd = np.stack([gd[i] for i, m in enumerate(L.DIAG_OUT) if m != "T2M"])
+    assert np.isfinite(got[L.s("STC")]).all()
+    ok = close(got, st, 1e-9, 1e-9).all(0) & close(gd, od, 1e-9, 1e-9).all(0) & \
+        (cs.isnow.cpu().numpy()[idx] == isn)
+    assert ok.mean() >= 0.99, column_mismatch(got, st, 1e-9, 1e-9, STATE_NAMES)[1][:8]
+
+
 def test_bench_window_bit_exact_vs_oracle(engines, oracle_port):
     """The workload bench.py times, as the driver runs it (`--steps 20
     --warmup 5`): config #3's 1,048,576 mixed columns in the coherent order,
