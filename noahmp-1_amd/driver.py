@@ -353,14 +353,9 @@ class OfflineDriver:
                     d = self.diag
                 if rank == 0:
                     os.makedirs(cfg.outdir, exist_ok=True)
-                    if self.grid is not None:
-                        path = ncio.ldasout_path(cfg.outdir, t1)
-                        ncio.write_ldasout(path, self.grid, self.to_grid_order(d.cpu().numpy()),
-                                           t1)
-                    else:
-                        path = os.path.join(cfg.outdir, f"{_stamp(t1)}.LDASOUT.npz")
-                        np.savez(path, time=np.array(t1.isoformat()),
-                                 fields=np.array(",".join(L.DIAG_OUT)), diag=d.cpu().numpy())
+                    path = (ncio.ldasout_path(cfg.outdir, t1) if self.grid is not None else
+                            os.path.join(cfg.outdir, f"{_stamp(t1)}.LDASOUT.npz"))
+                    self._write_output(d, path, t1)
                     self.written.append(path)
             self.phase_s["output"] += time.perf_counter() - tp
             if _is_boundary(t1, cfg.begdatetime, res_every) and self.write:
@@ -370,4 +365,44 @@ class OfflineDriver:
                 self.save_restart(os.path.join(cfg.resdir, name))
         self.ranges.join()
         torch.cuda.synchronize(self.dev)
+        self.flush_output()
         return self
+
+    # ---- output -----------------------------------------------------------------
+    def _write_output(self, d: torch.Tensor, path: str, t1: datetime.datetime):
+        """One output step's (16, n) fluxes, written on a background thread:
+        d is copied into one of two pinned host buffers on the current stream
+        (after the step that produced it), and the writer thread waits for the
+        copy, restores the grid order and writes the file while the loop goes
+        on stepping.  A buffer is reused once its previous file is written."""
+        if getattr(self, "_writer", None) is None:
+            from concurrent.futures import ThreadPoolExecutor
+            self._writer = ThreadPoolExecutor(1)
+            self._out_host, self._out_fut, self._n_out_w = [None, None], [None, None], 0
+        k = self._n_out_w % 2
+        self._n_out_w += 1
+        if self._out_fut[k] is not None:
+            self._out_fut[k].result()
+        h = self._out_host[k]
+        if h is None or h.shape != d.shape or h.dtype != d.dtype:
+            h = self._out_host[k] = torch.empty(d.shape, dtype=d.dtype, pin_memory=True)
+        h.copy_(d, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(self.dev))
+
+        def job():
+            ev.synchronize()
+            a = h.numpy()
+            if self.grid is not None:
+                ncio.write_ldasout(path, self.grid, self.to_grid_order(a), t1)
+            else:
+                np.savez(path, time=np.array(t1.isoformat()),
+                         fields=np.array(",".join(L.DIAG_OUT)), diag=a)
+        self._out_fut[k] = self._writer.submit(job)
+
+    def flush_output(self):
+        """Wait until every output file issued so far is written (raises a
+        writer's error)."""
+        for f in getattr(self, "_out_fut", ()):
+            if f is not None:
+                f.result()

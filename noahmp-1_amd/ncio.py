@@ -308,13 +308,28 @@ class LdasinForcing:
         k = (t - self.begin) // self.every
         return self.begin + k * self.every
 
+    def _load(self, ti: datetime.datetime) -> dict:
+        raw = read_ldasin(ldasin_path(self.indir, ti))
+        return {k: self.grid.columns(v)[self.cols] for k, v in raw.items()}
+
     def fields(self, t: datetime.datetime) -> dict:
-        """The LDASIN variables of the step starting at t (this rank's columns)."""
+        """The LDASIN variables of the step starting at t (this rank's columns).
+        The next input time's file is read ahead on a background thread while
+        the steps of this one run (a missing next file only fails when a
+        step needs it)."""
         ti = self.input_time(t)
         if ti != self._t:
-            raw = read_ldasin(ldasin_path(self.indir, ti))
-            self._fields = {k: self.grid.columns(v)[self.cols] for k, v in raw.items()}
+            ahead = getattr(self, "_ahead", None)
+            if ahead is not None and ahead[0] == ti:
+                self._fields = ahead[1].result()
+            else:
+                self._fields = self._load(ti)
             self._t = ti
+            if getattr(self, "_reader", None) is None:
+                from concurrent.futures import ThreadPoolExecutor
+                self._reader = ThreadPoolExecutor(1)
+            nxt = ti + self.every
+            self._ahead = (nxt, self._reader.submit(self._load, nxt))
         return self._fields
 
     def _chunks(self, fill):

@@ -13,6 +13,9 @@ timeout -k 10 400 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout
 rc=$?; tail -3 "$O/pytest_new.log"; [ $rc -eq 0 ] || { echo "pytest rc=$rc"; exit $rc; }
 TAG=${TAG:-r06c}/dist8 bash tools/dist_rehearsal8.sh > "$O/dist8.txt" 2>&1
 rc=$?; cat "$O/dist8.txt"; [ $rc -eq 0 ] || { echo "rehearsal rc=$rc"; exit $rc; }
+timeout -k 10 600 python -u tools/offline_timing.py --out "$O/offline_driver.json" \
+  > "$O/offline_timing.log" 2>&1 || { echo "offline timing failed"; tail -8 "$O/offline_timing.log"; exit 1; }
+grep '^{' "$O/offline_timing.log"
 MARKS="3 4 5 6 14 9 10 11 13 99" TAG=${TAG:-r06c}/phase bash tools/phase_counters.sh || exit 1
 cd "$R" && python tools/phase_counters.py "$O/phase" --out "$O/phase_counters.json"
 echo done
