@@ -138,6 +138,10 @@ def parse():
                          "all-gathers to every rank, north_star's single RCCL all-gather over "
                          "xGMI at output steps; 'root' gathers to rank 0 only, the rank that "
                          "writes LDASOUT (what the offline driver does)")
+    ap.add_argument("--gather-dtype", default="native", choices=("native", "f32"),
+                    help="type of the gathered fluxes for N > 1: the engine's ('native'), or "
+                         "f32 (the reference's output precision: half the link bytes of an "
+                         "fp64 run; the state stays fp64)")
     ap.add_argument("--period", type=int, default=48, help="resident forcing slices (cycled)")
     ap.add_argument("--forcing", default="resident", choices=("resident", "device"),
                     help="resident: --period host-generated forcing slices held in HBM and "
@@ -403,7 +407,8 @@ def main():
         # double-buffered output-step gather; a receiving rank's engine writes
         # straight into its own slot of the gather buffer (no local copy)
         gat = shard.DiagGather(L.NDIAG_OUT, world * n, dtype, dev, dst=gather_dst, comm=comm,
-                               force_collective=a.force_collective)
+                               force_collective=a.force_collective,
+                               wire_dtype=torch.float32 if a.gather_dtype == "f32" else None)
         sched = shard.OutputSchedule(a.out_every, gat, streams=ranges.streams)
     else:
         gat = None
@@ -511,6 +516,9 @@ def main():
                        "emulated_rank": a.emulate_rank,
                        "force_collective": a.force_collective or None,
                        "gather": a.gather if use_dist else None,
+                       "gather_dtype": (a.gather_dtype if a.gather_dtype != "native" else
+                                        ("f32" if a.precision == 4 else "f64"))
+                       if use_dist else None,
                        "backend": backend if use_dist else None},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,

@@ -78,10 +78,15 @@ class DiagGather:
 
     def __init__(self, nfield: int, ncol_total: int, dtype, device, dst: int | None = 0,
                  nbuf: int = 2, group=None, comm: torch.cuda.Stream | None = None,
-                 force_collective: bool = False):
+                 force_collective: bool = False, wire_dtype=None):
         """force_collective: issue the collective even on a single rank (where
         nothing needs to move), so the RCCL code path of a multi-GPU run can
-        be executed and checked on one GPU (tests/probe_rccl_gather.py)."""
+        be executed and checked on one GPU (tests/probe_rccl_gather.py).
+        wire_dtype: the gathered values' type when it differs from the
+        engine's `dtype` (e.g. fp32 fluxes of an fp64 run, half the link
+        bytes): the engine writes `local(b)` in dtype, `start` converts it
+        into the wire buffer on the issuing stream, `assemble` returns
+        wire_dtype."""
         self.force_collective = bool(force_collective)
         self.group = group
         self.world = dist.get_world_size(group)
@@ -95,9 +100,13 @@ class DiagGather:
         self.receives = dst is None or self.rank == dst
         self.staged = dist.get_backend(group) == "gloo" and self.device.type == "cuda"
         nslot = self.world if self.receives else 1
-        self.bufs = [torch.zeros(nslot * self.slot, dtype=dtype, device=self.device)
+        wire = dtype if wire_dtype is None else wire_dtype
+        self.bufs = [torch.zeros(nslot * self.slot, dtype=wire, device=self.device)
                      for _ in range(nbuf)]
-        self.host = [torch.zeros(nslot * self.slot, dtype=dtype) for _ in range(nbuf)] \
+        # engine-precision blocks the engine writes when the wire type differs
+        self.src = [torch.zeros((nfield, self.n_local), dtype=dtype, device=self.device)
+                    for _ in range(nbuf)] if wire != dtype else None
+        self.host = [torch.zeros(nslot * self.slot, dtype=wire) for _ in range(nbuf)] \
             if self.staged else None
         self.comm = comm
         self.pending = [None] * nbuf   # host-side work handles (CPU buffers)
@@ -107,9 +116,18 @@ class DiagGather:
     def _slot(self, buf: torch.Tensor, r: int) -> torch.Tensor:
         return buf[r * self.slot:(r + 1) * self.slot]
 
-    def local(self, b: int) -> torch.Tensor:
+    def _own(self, b: int) -> torch.Tensor:
         own = self._slot(self.bufs[b], self.rank if self.receives else 0)
         return own[:self.nfield * self.n_local].view(self.nfield, self.n_local)
+
+    def local(self, b: int) -> torch.Tensor:
+        return self.src[b] if self.src is not None else self._own(b)
+
+    def _convert(self, b: int):
+        """(wire_dtype differs) the engine's block into the wire buffer, on the
+        current stream."""
+        if self.src is not None:
+            self._own(b).copy_(self.src[b])
 
     def start(self, b: int, producers=()):
         """Issue the gather of buffer b after every stream in `producers` (e.g.
@@ -119,11 +137,18 @@ class DiagGather:
         bench, the collective's kernel taking CUs from the step)."""
         if self.world == 1 and not self.force_collective:
             self.local_producers[b] = list(producers)  # assemble() waits for them
+            if self.src is not None:
+                if self.device.type == "cuda":
+                    for s in producers:
+                        torch.cuda.current_stream(self.device).wait_stream(s)
+                self._convert(b)
+                self.local_producers[b] = []
             return
         bufs = self.host if self.staged else self.bufs
         if self.staged:
             for s in producers:
                 torch.cuda.current_stream(self.device).wait_stream(s)
+            self._convert(b)
             bufs[b].copy_(self.bufs[b])
             self._issue(b, bufs[b], async_op=False)
             if self.receives:
@@ -133,12 +158,14 @@ class DiagGather:
             for s in producers:
                 self.comm.wait_stream(s)
             with torch.cuda.stream(self.comm):
+                self._convert(b)
                 self._issue(b, bufs[b], async_op=True)
                 self._fence(b)
         else:
             if self.device.type == "cuda":
                 for s in producers:
                     torch.cuda.current_stream(self.device).wait_stream(s)
+            self._convert(b)
             self._issue(b, bufs[b], async_op=True)
             self._fence(b)
 

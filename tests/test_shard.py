@@ -112,6 +112,48 @@ def test_gloo_output_loop_equals_single_rank(oracle_port, tmp_path, world, ncol,
     assert np.array_equal(got.view(np.int32), want.view(np.int32))
 
 
+def _wire_worker(rank, world, port, out_path):
+    """A rank whose engine writes fp64 fluxes gathered as fp32 (DiagGather
+    wire_dtype): two output steps through OutputSchedule, both buffers."""
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root]
+    import noahmp_pkg  # noqa: F401
+    from noahmp_amd import shard as sh
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    ncol = 1001
+    s0, cnt = sh.shard_range(ncol, rank, world)
+    gat = sh.DiagGather(L.NDIAG_OUT, ncol, torch.float64, "cpu", dst=None,
+                        wire_dtype=torch.float32)
+    sched = sh.OutputSchedule(1, gat)
+    got = []
+    for k in range(3):
+        d = sched.diag_for(k)
+        assert d.dtype == torch.float64 and d.shape == (L.NDIAG_OUT, cnt)
+        vals = torch.arange(L.NDIAG_OUT * ncol, dtype=torch.float64).view(L.NDIAG_OUT, ncol)
+        d.copy_(vals[:, s0:s0 + cnt] / 3.0 + k)
+        sched.finish(k)
+        got.append(gat.assemble(sched.buffer(k)).clone())
+    gat.wait_all()
+    if rank == 0:
+        np.save(out_path, torch.stack(got).numpy())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_gloo_gather_fp32_wire_of_fp64_fluxes(tmp_path):
+    """DiagGather(wire_dtype=float32): fp64 engine fluxes travel and arrive as
+    their fp32 rounding (bench.py --gather-dtype f32), ragged shards, world 3."""
+    out_path = str(tmp_path / "wire.npy")
+    mp.start_processes(_wire_worker, args=(3, _free_port(), out_path), nprocs=3,
+                       start_method="spawn")
+    got = np.load(out_path)
+    vals = np.arange(L.NDIAG_OUT * 1001, dtype=np.float64).reshape(L.NDIAG_OUT, 1001)
+    want = np.stack([(vals / 3.0 + k).astype(np.float32) for k in range(3)])
+    assert got.dtype == np.float32 and np.array_equal(got, want)
+
+
 def _gpu_worker(rank, world, port, out_path):
     """One rank of a world-size-2 run on the box's single GPU: the HIP engine
     steps this rank's column shard; the output diagnostics are gathered over
