@@ -71,6 +71,9 @@ def main():
         v["kernel_ms"], v["dispatches"] = kernel_ms(os.path.join(d, "kt"))
         cum[k] = v
     phases, prev = [], None
+    names = dict(NAMES)
+    if marks and marks[0] == 3:  # no mark 2 run: the first row holds the prelude too
+        names[3] = "prelude + df_top + radiation"
     for k in marks:
         c = cum[k]
         d = {x: c[x] - (prev[x] if prev else 0.0) for x in c if isinstance(c[x], float)}
@@ -83,7 +86,7 @@ def main():
         other = valu - f32 - f64 - tr - i32
         # SIMD cycles per wave64 instruction by class (bench.py VALU_CYCLES)
         wcyc = 2 * f32 + 4 * f64 + 8 * tr + 2 * i32 + 2 * other
-        ph = {"mark": k, "phase": NAMES.get(k, str(k)),
+        ph = {"mark": k, "phase": names.get(k, str(k)),
               "kernel_ms": d["kernel_ms"],
               "valu_per_wave": valu / waves,
               "lane_util": (d["SQ_THREAD_CYCLES_VALU"] / (64.0 * d["SQ_ACTIVE_INST_VALU"])
