@@ -1029,6 +1029,11 @@ static __device__ unsigned int nmp_fb_reason[32];
 #ifndef NMP_BARE_DIV
 #define NMP_BARE_DIV 1
 #endif
+// NMP_SOIL_DIV: the soil-water sub-steps' divisions by the layer thicknesses
+// (launch-uniform) with DivFast32, a tiny numerator on IEEE division
+#ifndef NMP_SOIL_DIV
+#define NMP_SOIL_DIV 1
+#endif
 #ifndef NMP_VEGE_UNROLL
 #define NMP_VEGE_UNROLL 1
 #endif
@@ -2755,6 +2760,51 @@ NMP_UNROLL(NMP_BARE_UNROLL)
     const T dtfine = DT / (T)niter;
     T qdrain_save = L(0.0);
     const T dwsat = (T)S.dwsat, dksat = (T)S.dksat;
+    // The sub-steps divide by the layer thicknesses TEMP1 = ZSOIL(K-1) -
+    // ZSOIL(K+1) and DENOM = ZSOIL(K-1) - ZSOIL(K) (srt, func.f90:6238-6276),
+    // launch-uniform.  In the fp32 "ref" option-set kernels these divisions
+    // use DivFast32 (one reciprocal per thickness for the whole step), which
+    // equals IEEE a/b for |b| in [2^-126, 2^126] (checked here once), a = 0
+    // or |a| >= 2^-102, and a normal quotient -- implied for |b| <= 2^24
+    // (tools/fdiv_exhaust.hip; tools/div_proof.py "soil water").  The
+    // numerators (WDF * DDZ of very dry soil, a cancelling WFLUX) can be
+    // tiny, so each division checks its own and a lane below 2^-102 takes
+    // IEEE division (an exec-masked branch no lane usually enters).
+#if NMP_SOIL_DIV
+    constexpr bool kSoilFast = sizeof(T) == 4 && R && OS != 0;
+#else
+    constexpr bool kSoilFast = false;
+#endif
+    typedef std::conditional_t<kSoilFast, DivFast32, DivRef<T>> SoilDiv;
+    const SoilDiv sd;
+    Recip<T> rtemp[3], rden[4], rnden[4];
+    bool soil_ok = true;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const T den = (k == 0) ? -zsoil[0] : (zsoil[k - 1] - zsoil[k]);
+      rden[k] = sd.rec(den);
+      rnden[k] = sd.rec(-den);
+      soil_ok = soil_ok & (fabs(den) >= L(0x1p-126)) & (fabs(den) <= L(0x1p+24));
+      if (k < 3) {
+        const T tmp = (k == 0) ? -zsoil[1] : (zsoil[k - 1] - zsoil[k + 1]);
+        rtemp[k] = sd.rec(tmp);
+        soil_ok = soil_ok & (fabs(tmp) >= L(0x1p-126)) & (fabs(tmp) <= L(0x1p+24));
+      }
+    }
+    auto sdv = [&](T a, const Recip<T>& rb) -> T {
+      if constexpr (kSoilFast) {
+        T q = sd.div(a, rb);
+        if (__builtin_expect(!soil_ok || (fabs(a) < L(0x1p-102) && a != L(0.0)), 0)) {
+          q = a / rb.b;
+#ifdef NMP_COUNT_FALLBACK
+          atomicAdd(&nmp_fb_reason[25], 1u);  // soil-water division on IEEE
+#endif
+        }
+        return q;
+      } else {
+        return a / rb.b;
+      }
+    };
 #pragma unroll 1
     for (int it = 1; it <= niter; ++it) {
       // srt: func.f90:6199-6305
@@ -2785,24 +2835,20 @@ NMP_UNROLL(NMP_BARE_UNROLL)
           smx[k] = c.sh2o[k];
         }
       }
-      T ddz[4], denom[4], dsmdz[4], wflux[4];
+      // DENOM(K) (:6238-6276) is rden[k].b
+      T ddz[4], dsmdz[4], wflux[4];
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         if (k == 0) {
-          denom[k] = -zsoil[k];
-          T temp1 = -zsoil[k + 1];
-          ddz[k] = L(2.0) / temp1;
-          dsmdz[k] = L(2.0) * (smx[k] - smx[k + 1]) / temp1;
+          ddz[k] = sdv(L(2.0), rtemp[k]);
+          dsmdz[k] = sdv(L(2.0) * (smx[k] - smx[k + 1]), rtemp[k]);
           wflux[k] = wdf[k] * dsmdz[k] + wcnd[k] - qinfil + etrani[k] + qseva;
         } else if (k < 3) {
-          denom[k] = (zsoil[k - 1] - zsoil[k]);
-          T temp1 = (zsoil[k - 1] - zsoil[k + 1]);
-          ddz[k] = L(2.0) / temp1;
-          dsmdz[k] = L(2.0) * (smx[k] - smx[k + 1]) / temp1;
+          ddz[k] = sdv(L(2.0), rtemp[k]);
+          dsmdz[k] = sdv(L(2.0) * (smx[k] - smx[k + 1]), rtemp[k]);
           wflux[k] = wdf[k] * dsmdz[k] + wcnd[k] - wdf[k - 1] * dsmdz[k - 1] - wcnd[k - 1] +
                      etrani[k];
         } else {
-          denom[k] = (zsoil[k - 1] - zsoil[k]);
           if (o.run == 1 || o.run == 2) qdrain = L(0.0);
           if (o.run == 3) qdrain = (T)P.g.slope[c.slptyp - 1] * wcnd[k];
           if (o.run == 4) qdrain = (L(1.0) - fcrmax) * wcnd[k];
@@ -2816,18 +2862,18 @@ NMP_UNROLL(NMP_BARE_UNROLL)
       for (int k = 0; k < 4; ++k) {
         if (k == 0) {
           ai[k] = L(0.0);
-          bi[k] = wdf[k] * ddz[k] / denom[k];
+          bi[k] = sdv(wdf[k] * ddz[k], rden[k]);
           ci[k] = -bi[k];
         } else if (k < 3) {
-          ai[k] = -wdf[k - 1] * ddz[k - 1] / denom[k];
-          ci[k] = -wdf[k] * ddz[k] / denom[k];
+          ai[k] = sdv(-wdf[k - 1] * ddz[k - 1], rden[k]);
+          ci[k] = sdv(-wdf[k] * ddz[k], rden[k]);
           bi[k] = -(ai[k] + ci[k]);
         } else {
-          ai[k] = -wdf[k - 1] * ddz[k - 1] / denom[k];
+          ai[k] = sdv(-wdf[k - 1] * ddz[k - 1], rden[k]);
           ci[k] = L(0.0);
           bi[k] = -(ai[k] + ci[k]);
         }
-        rhstt[k] = wflux[k] / (-denom[k]);
+        rhstt[k] = sdv(wflux[k], rnden[k]);
       }
       // sstep: func.f90:6308-6383
       T ciin[4], rin[4], pp[4], del[4];

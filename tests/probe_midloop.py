@@ -9,7 +9,9 @@ the first iteration's stomata outputs.  Those lanes re-run the loop with IEEE
 division from restored inputs (sflx_kernel.hip vege_loop / bare_loop).  Every
 column must still equal the C restatement of the reference bit for bit, in
 both occupancy instantiations and at diagnostics levels NONE and FULL, and
-the device counter must show the in-loop windows fired.
+the device counter must show the in-loop windows fired.  A dry-clay set sends
+soil-water sub-step divisions (NMP_SOIL_DIV) below DivFast32's exact region:
+they must take IEEE division (counted) and stay bit-exact.
 
     NOAHMP_ENGINE_LIB=.../lib_probe_midloop.so python tests/probe_midloop.py
 
@@ -82,6 +84,39 @@ def main():
                        "columns_differing": int((~ok).sum())}
                 res["runs"].append(run)
                 ok_all = ok_all and bool(ok.all() and fb > 0 and why[19] > 0 and why[20] > 0)
+    # soil water (NMP_SOIL_DIV): very dry clay (SOILTYP 12, BEXP 11.55) makes
+    # WDF * DDZ fall below 2^-102, outside DivFast32's exact region: those
+    # divisions must take IEEE division (fb_reason[25]) and every column keep
+    # the reference's bits
+    for seed in (41,):
+        cols = cases.make_columns(n, "mixed", P.as_dict(), seed=seed, julian=180.0)
+        dry = np.arange(n) % 2 == 0
+        si = cols.static_i
+        si[L.STATIC_I.index("SOILTYP")][dry] = 12
+        for fld in ("SH2O", "SMC"):
+            st = cols.state[L.s(fld)]
+            st[:, dry] = np.float32(0.001) + np.float32(0.0001) * np.arange(4)[:, None]
+        f = cases.forcing_step(cols, jul, yl, 0, seed=seed)
+        est, eisn, edg, _ = port.step(load_params(), tuple(opts), cases.CASE_NML_ZSOIL, dt, yl,
+                                      jul, cols.state, cols.isnow, cols.static_f, cols.static_i, f)
+        for variant in ("small", "full"):
+            eng = Engine(P, L.CASE_NML_OPTIONS, device=0)
+            assert eng.launch_variant(variant) == variant
+            cs = ColumnState.from_host(cols, "cuda:0")
+            raw.nmp_debug_fallback_count(1, None)
+            diag = torch.zeros((L.NDIAG_FULL, n), device="cuda:0")
+            eng.step(cs, torch.as_tensor(f, device="cuda:0"), cases.CASE_NML_ZSOIL, dt, jul, yl,
+                     diag, L.DIAG_FULL_LEVEL)
+            torch.cuda.synchronize()
+            why = np.zeros(32, np.uint32)
+            raw.nmp_debug_fallback_count(1, why.ctypes.data)
+            ok = bit_equal(cs.state.cpu().numpy(), est).all(0) & \
+                (cs.isnow.cpu().numpy() == eisn) & bit_equal(diag.cpu().numpy(), edg).all(0)
+            eng.close()
+            run = {"seed": seed, "variant": variant, "case": "dry clay",
+                   "soil_ieee_divisions": int(why[25]), "columns_differing": int((~ok).sum())}
+            res["runs"].append(run)
+            ok_all = ok_all and bool(ok.all() and why[25] > 0)
     res["ok"] = ok_all
     print(json.dumps(res))
     return 0 if ok_all else 1

@@ -42,6 +42,8 @@ VARIANTS = {
     "w5": ("-DNMP_WAVES_PER_EU=5",),
     "d1": ("-DNMP_WAVES_PER_EU_F64=1",),
     "w2_d1": ("-DNMP_WAVES_PER_EU=2", "-DNMP_WAVES_PER_EU_F64=1"),
+    # round 6: the soil-water sub-steps' divisions on IEEE only (A/B of NMP_SOIL_DIV)
+    "soildiv0": {"f32": ["-DNMP_SOIL_DIV=0"]},
     # per-phase truncation at a run-time mark (tools/phase_counters.sh)
     "trunc": ("-DNMP_TRUNC_RUNTIME",),
     "en_w4": ("-DNMP_TRUNC_ENERGY",),
