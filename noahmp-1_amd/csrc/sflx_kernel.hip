@@ -2764,12 +2764,13 @@ NMP_UNROLL(NMP_BARE_UNROLL)
     // ZSOIL(K+1) and DENOM = ZSOIL(K-1) - ZSOIL(K) (srt, func.f90:6238-6276),
     // launch-uniform.  In the fp32 "ref" option-set kernels these divisions
     // use DivFast32 (one reciprocal per thickness for the whole step), which
-    // equals IEEE a/b for |b| in [2^-126, 2^126] (checked here once), a = 0
-    // or |a| >= 2^-102, and a normal quotient -- implied for |b| <= 2^24
-    // (tools/fdiv_exhaust.hip; tools/div_proof.py "soil water").  The
-    // numerators (WDF * DDZ of very dry soil, a cancelling WFLUX) can be
-    // tiny, so each division checks its own and a lane below 2^-102 takes
-    // IEEE division (an exec-masked branch no lane usually enters).
+    // equals IEEE a/b for |b| in [2^-126, 2^126], a = 0 or |a| >= 2^-102, and
+    // a normal quotient (tools/fdiv_exhaust.hip).  The thicknesses are checked
+    // here once against [2^-20, 2^20]; the numerators (WDF * DDZ of very dry
+    // soil is ~1e-32, WFLUX may cancel) are checked per division against
+    // a = 0 or [2^-102, 2^100], so the quotient lies in [2^-122, 2^120]
+    // (tools/div_proof.py soil_sites).  A lane outside takes IEEE division
+    // (an exec-masked branch that no lane usually enters).
 #if NMP_SOIL_DIV
     constexpr bool kSoilFast = sizeof(T) == 4 && R && OS != 0;
 #else
@@ -2784,17 +2785,19 @@ NMP_UNROLL(NMP_BARE_UNROLL)
       const T den = (k == 0) ? -zsoil[0] : (zsoil[k - 1] - zsoil[k]);
       rden[k] = sd.rec(den);
       rnden[k] = sd.rec(-den);
-      soil_ok = soil_ok & (fabs(den) >= L(0x1p-126)) & (fabs(den) <= L(0x1p+24));
+      soil_ok = soil_ok & (fabs(den) >= L(0x1p-20)) & (fabs(den) <= L(0x1p+20));
       if (k < 3) {
         const T tmp = (k == 0) ? -zsoil[1] : (zsoil[k - 1] - zsoil[k + 1]);
         rtemp[k] = sd.rec(tmp);
-        soil_ok = soil_ok & (fabs(tmp) >= L(0x1p-126)) & (fabs(tmp) <= L(0x1p+24));
+        soil_ok = soil_ok & (fabs(tmp) >= L(0x1p-20)) & (fabs(tmp) <= L(0x1p+20));
       }
     }
     auto sdv = [&](T a, const Recip<T>& rb) -> T {
       if constexpr (kSoilFast) {
         T q = sd.div(a, rb);
-        if (__builtin_expect(!soil_ok || (fabs(a) < L(0x1p-102) && a != L(0.0)), 0)) {
+        const T m = fabs(a);
+        const bool in = a == L(0.0) || (m >= L(0x1p-102) && m <= L(0x1p+100));  // NaN: out
+        if (__builtin_expect(!soil_ok || !in, 0)) {
           q = a / rb.b;
 #ifdef NMP_COUNT_FALLBACK
           atomicAdd(&nmp_fb_reason[25], 1u);  // soil-water division on IEEE

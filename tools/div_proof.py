@@ -1,4 +1,5 @@
-"""Range proof of the canopy Newton loop's short divisions (DivFast32).
+"""Range proof of the short divisions (DivFast32) in the canopy and bare-ground
+Newton loops, the stomata bisection and the soil-water sub-steps.
 
 DivFast32 (csrc/sflx_math.h) returns IEEE a/b bit for bit when
   b is normal with a normal reciprocal: |b| in [2^-126, 2^126],
@@ -218,6 +219,24 @@ def stomata_sites(D, T, p, es, rb):
             bad.append(name)
 
 
+def soil_sites():
+    """The soil-water sub-steps' divisions by the layer thicknesses (srt,
+    func.f90:6238-6276; sflx_kernel.hip NMP_SOIL_DIV).  Their denominators are
+    launch-uniform differences of ZSOIL, which the kernel checks once against
+    [2^-20, 2^20] (outside: every such division on IEEE).  Their numerators
+    (2, 2*(SMX(K)-SMX(K+1)), WDF*DDZ, WFLUX) are not bounded away from 0 --
+    WDF of very dry clay is ~1e-32 -- so the kernel checks each numerator at
+    run time: a = 0 or 2^-102 <= |a| <= 2^100, else that lane divides on IEEE.
+    Inside both checks the quotient lies in [2^-122, 2^120]."""
+    den = M(2.0 ** -20, 2.0 ** 20)
+    num = M(A_MIN * (1 + 2 * W), 2.0 ** 100, True)  # (M widens its bounds by W)
+    note = "numerator window checked per lane, IEEE outside"
+    site("soil: DDZ = 2 / TEMP1", c(2.0), den, ":6243")
+    site("soil: DSMDZ = 2*(SMX(K)-SMX(K+1)) / TEMP1", num, den, ":6244", note)
+    site("soil: AI, CI, BI = -WDF*DDZ / DENOM", num, den, ":6266-6272", note)
+    site("soil: RHSTT = WFLUX / (-DENOM)", num, den, ":6275", note)
+
+
 def main():
     D = domain()
     # ---- loop-invariant inputs: the kernel's entry check (vege_domain.h) ----
@@ -357,6 +376,7 @@ def main():
     site("bare: CEV = (...) / (RSURF+RAWB)", cevi, M(rahb.lo, rahb.hi + rsurf_hi), ":3187")
 
     stomata_sites(D, T, p, es, rb)
+    soil_sites()
 
     # ---- induction: the iteration ends inside the intervals it started from ----
     assert h_q.hi <= h.hi * 1.001 and h_q.lo >= h.lo * 0.999, (h_q, h)
