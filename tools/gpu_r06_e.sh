@@ -7,7 +7,7 @@
 set -u
 R="${GRAFT_REPO_ROOT:-/root/repo}"
 cd "$R"
-O=gpurun_out/${TAG:-r06e}
+O=$R/gpurun_out/${TAG:-r06e}
 mkdir -p "$O"
 export PYTHONUNBUFFERED=1
 step() {  # name seconds cmd...
@@ -22,12 +22,15 @@ if [ "${SKIP_TESTS:-0}" != 1 ]; then
   step pytest_all 600 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread
   step smoke 120 python -c "import __graft_entry__ as g; g.smoke()"
 fi
-step bench_driver 300 python -u bench.py --steps 20 --warmup 5
-TAG=${TAG:-r06e}/pmc step pmc 900 bash tools/pmc_run.sh
-step traffic 60 python tools/pmc_traffic.py "$O/pmc" --out "$O/traffic.json"
+if [ "${SKIP_PMC:-0}" != 1 ]; then
+  step bench_driver 300 python -u bench.py --steps 20 --warmup 5
+  TAG=${TAG:-r06e}/pmc step pmc 900 bash tools/pmc_run.sh
+  step traffic 60 python tools/pmc_traffic.py "$O/pmc" --out "$O/traffic.json"
+fi
 cd /tmp && export TMPDIR=/tmp
-step ktrace 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/$O/ktrace" -o run -- python3 "$R/bench.py" --steps 20 --warmup 5 --no-cpu-baseline
+step ktrace 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/ktrace" -o run -- python3 "$R/bench.py" --steps 20 --warmup 5 --no-cpu-baseline
 cd "$R"
+step bench_with_traffic 300 python -u bench.py --steps 20 --warmup 5 --no-cpu-baseline
 step bench_48 300 python -u bench.py --no-cpu-baseline
 if [ "${CONFIGS:-1}" = 1 ]; then
   TAG=${TAG:-r06e}/configs step configs 900 bash tools/configs.sh
