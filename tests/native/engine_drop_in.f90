@@ -7,6 +7,9 @@
 ! oracle/Makefile), then either
 !   mode "run" : noahmp_init once, noahmp_run every step over the module's
 !                column arrays (state resident on the device), or
+!   mode "runl": as "run", with the step's LDASIN block (nmp_ldasin, taken
+!                from the forcing's T2D Q2D U2D V2D PSFC RAINRATE SWDOWN LWDOWN
+!                COSZ) and nmp_ldasin_forcing, the forcing formed on the device;
 !   mode "sflx": one noahmp_sflx call per column per step with the
 !                reference's 131 arguments (FICEOLD from the step-start ice
 !                fraction, as the reference harness passes it).
@@ -18,11 +21,12 @@
 ! every <out_every>-th step and level 0 otherwise, arrays page-locked or not
 ! (<pinned> 1|0).  Writes one line to <out>: ncol nsteps out_every pinned
 ! ms_per_run ms_per_fill column_steps_per_s bytes_up_per_step bytes_down_per_step
-! chunks.
+! chunks ldasin.
 !
-! usage: engine_drop_in <run|sflx> <tbl_dir> <in.bin> <out.bin>
+! usage: engine_drop_in <run|runl|sflx> <tbl_dir> <in.bin> <out.bin>
 !        engine_drop_in time <tbl_dir> <in.bin> <out.txt> <ncol> <nsteps> <out_every> <pinned>
 !                            [<chunks>]   (noahmp_run's pipeline chunks, default the module's)
+!                            [<ldasin>]   (1: upload the LDASIN block, nmp_ldasin_forcing)
 !   in.bin : int32 n, nsteps, yearlen, options(12); real zsoil(4), dt;
 !            real julian(nsteps); int32 static_i(n,6), isnow(n);
 !            real static_f(n,6), state(n,56), forcing(n,12,nsteps)
@@ -38,6 +42,8 @@ program engine_drop_in
   real :: zs(4), dt
   real, allocatable :: jul(:), sf(:,:), st(:,:), frc(:,:,:)
   integer, allocatable :: si(:,:), isn(:)
+  ! LDASIN field f (NMP_L_* + 1) = forcing field lmap(f) (NMP_A_* + 1)
+  integer, parameter :: lmap(9) = [1, 6, 4, 5, 3, 9, 7, 8, 10]
 
   call get_command_argument(1, mode)
   call get_command_argument(2, tbl)
@@ -64,8 +70,13 @@ program engine_drop_in
   open(newunit=v, file=trim(fout), access='stream', form='unformatted', status='replace')
   do s = 1, nsteps
      nmp_julian = jul(s)
-     if (trim(mode) == 'run') then
-        nmp_forcing = frc(:, :, s)
+     if (trim(mode) == 'run' .or. trim(mode) == 'runl') then
+        nmp_ldasin_forcing = trim(mode) == 'runl'
+        if (nmp_ldasin_forcing) then
+           nmp_ldasin = frc(:, lmap, s)
+        else
+           nmp_forcing = frc(:, :, s)
+        end if
         call noahmp_run()
         call noahmp_get_state()
      else
@@ -83,9 +94,9 @@ contains
 
   subroutine time_run()   ! mode "time": noahmp_run at a production column count
     character(len=64) :: arg
-    integer :: ncol, nt, oe, pinned, nf, k, i, j
+    integer :: ncol, nt, oe, pinned, nf, k, i, j, ldasin
     integer(8) :: t0, t1, t2, rate, trun, tfill
-    real, allocatable :: frep(:,:,:)
+    real, allocatable :: frep(:,:,:), lrep(:,:,:)
     real(8) :: ms_run, ms_fill, up, down
     call get_command_argument(5, arg); read(arg, *) ncol
     call get_command_argument(6, arg); read(arg, *) nt
@@ -94,6 +105,11 @@ contains
     if (command_argument_count() >= 9) then
        call get_command_argument(9, arg); read(arg, *) nmp_chunks
     end if
+    ldasin = 0
+    if (command_argument_count() >= 10) then
+       call get_command_argument(10, arg); read(arg, *) ldasin
+    end if
+    nmp_ldasin_forcing = ldasin /= 0
     nf = min(nsteps, 4)
     call noahmp_columns(ncol)
     do i = 1, ncol
@@ -101,11 +117,12 @@ contains
        nmp_static_i(i, :) = si(j, :); nmp_isnow(i) = isn(j)
        nmp_static_f(i, :) = sf(j, :); nmp_state(i, :) = st(j, :)
     end do
-    allocate(frep(ncol, 12, nf))
+    allocate(frep(ncol, 12, nf), lrep(ncol, 9, nf))
     do k = 1, nf
        do i = 1, ncol
           frep(i, :, k) = frc(mod(i - 1, n) + 1, :, k)
        end do
+       lrep(:, :, k) = frep(:, lmap, k)
     end do
     nmp_zsoil = zs; nmp_dt = dt; nmp_yearlen = yl
     nmp_pinned = pinned /= 0
@@ -116,7 +133,11 @@ contains
     do s = 1, nt + 2
        k = mod(s - 1, nf) + 1
        call system_clock(t0)
-       nmp_forcing = frep(:, :, k)          ! the host's own work: filling this step's forcing
+       if (nmp_ldasin_forcing) then         ! the host's own work: filling this step's forcing
+          nmp_ldasin = lrep(:, :, k)
+       else
+          nmp_forcing = frep(:, :, k)
+       end if
        nmp_julian = jul(k)
        nmp_diag_level = merge(1, 0, mod(s, oe) == 0)
        call system_clock(t1)
@@ -124,8 +145,8 @@ contains
        call system_clock(t2)
        if (s > 2) then
           tfill = tfill + (t1 - t0); trun = trun + (t2 - t1)
-          up = up + 4d0 * 12 * ncol
-          down = down + 4d0 * ncol * (1 + merge(16, 0, nmp_diag_level == 1))
+          up = up + merge(4d0 * 9, storage_size(nmp_forcing) / 8d0 * 12, nmp_ldasin_forcing) * ncol
+          down = down + ncol * (4d0 + storage_size(nmp_diag) / 8d0 * merge(16, 0, nmp_diag_level == 1))
        end if
     end do
     call noahmp_get_state()
@@ -133,8 +154,8 @@ contains
     ms_fill = 1d3 * real(tfill, 8) / real(rate, 8) / nt
     open(newunit=v, file=trim(fout), status='replace')
     write(v, '(i0, 1x, i0, 1x, i0, 1x, i0, 1x, es14.6, 1x, es14.6, 1x, es14.6, 1x, es14.6, 1x, es14.6, &
-         & 1x, i0)') ncol, nt, oe, pinned, ms_run, ms_fill, ncol / (ms_run * 1d-3), up / nt, down / nt, &
-         nmp_chunks
+         & 1x, i0, 1x, i0)') ncol, nt, oe, pinned, ms_run, ms_fill, ncol / (ms_run * 1d-3), up / nt, &
+         down / nt, nmp_chunks, ldasin
     close(v)
     call noahmp_finalize()
   end subroutine

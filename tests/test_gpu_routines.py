@@ -407,6 +407,54 @@ def test_fortran_engine_slot_vs_reference(mode):
 
 
 @pytest.mark.gpu
+def test_fortran_engine_slot_ldasin_block(tmp_path):
+    """The engine slot's LDASIN-block upload (`nmp_ldasin_forcing`): mode
+    "runl" fills `nmp_ldasin` (the fixture forcing's T2D Q2D U2D V2D PSFC
+    RAINRATE SWDOWN LWDOWN COSZ) and noahmp_run forms the forcing on the device
+    with nmp_forcing_from_ldasin.  Its 96-step trajectory equals, bit for bit,
+    mode "run" (12 fields uploaded) on the forcing an HRLDAS host forms from
+    the same variables: SFCPRS = PSFC, CO2AIR = 395e-6 PSFC, O2AIR = 0.209 PSFC
+    rounded to fp32 (noahmp-1_amd/ncio.py LdasinForcing, after
+    hrldas_drv_HRLDAS.f90's CO2/O2 volume fractions)."""
+    import subprocess
+    from golden_io import load
+    from noahmp_amd import layout as L
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    exe = os.path.join(root, "tests", "lib", "engine_drop_in")
+    tbl = os.path.join(root, "oracle", "_ref", "tbl")
+    if not os.path.exists(exe):
+        pytest.fail(f"{exe} missing: run __graft_entry__.build() where /root/reference exists")
+    if not os.path.isdir(tbl):
+        pytest.skip("no TBL files beside the oracle (oracle/_ref/tbl) for nmp_read_tables")
+    g = load("traj_casenml.npz")
+    n, nsteps = g["isnow0"].shape[0], g["forcing"].shape[0]
+    dt = float(g["dt"])
+    jul = np.array([float(g["julian0"]) + s * dt / 86400.0 for s in range(nsteps)], np.float32)
+    frc = np.array(g["forcing"], np.float32)          # (nsteps, 12, n)
+    a = {k: L.FORCING.index(k) for k in ("SFCPRS", "PSFC", "CO2AIR", "O2AIR")}
+    psfc = frc[:, a["PSFC"]].astype(np.float64)
+    host = frc.copy()
+    host[:, a["SFCPRS"]] = frc[:, a["PSFC"]]
+    host[:, a["CO2AIR"]] = (395.0e-6 * psfc).astype(np.float32)
+    host[:, a["O2AIR"]] = (0.209 * psfc).astype(np.float32)
+    outs = {}
+    for mode, forcing in (("runl", frc), ("run", host)):
+        fin, fout = str(tmp_path / f"{mode}.in"), str(tmp_path / f"{mode}.out")
+        with open(fin, "wb") as f:
+            for a in (np.array([n, nsteps, int(g["yearlen"])], np.int32),
+                      g["options"].astype(np.int32), g["zsoil"].astype(np.float32),
+                      np.array([dt], np.float32), jul, g["static_i"].astype(np.int32),
+                      g["isnow0"].astype(np.int32), g["static_f"], g["state0"], forcing):
+                f.write(np.ascontiguousarray(a).tobytes())
+        r = subprocess.run([exe, mode, tbl, fin, fout], capture_output=True, text=True,
+                           timeout=300)
+        assert r.returncode == 0, r.stdout + r.stderr
+        outs[mode] = np.fromfile(fout, np.uint8)
+    assert outs["runl"].size == nsteps * 4 * n * (56 + 1 + 58 + 1)
+    assert np.array_equal(outs["runl"], outs["run"])
+
+
+@pytest.mark.gpu
 def test_fortran_engine_slot_fp64(tmp_path):
     """INTEGRATION.md's engine slot with its one-line switch to the fp64
     engine (`nmp_rk = c_double`, tests/lib/engine_drop_in_f64): noahmp_init /

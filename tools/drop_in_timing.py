@@ -8,7 +8,9 @@ INTEGRATION.md) at --ncol columns (the set replicated) for --steps timed
 noahmp_run calls, with the module's arrays page-locked or pageable, and the
 16 output fluxes copied back every step or every 6th step (the namelist's
 3-hour output at dt = 1800 s), and noahmp_run pipelined over 1-8 column
-chunks.  Prints one JSON line per configuration and writes them all to --out.
+chunks, with the 12 forcing fields uploaded or the 9-field LDASIN block
+(`nmp_ldasin_forcing`, the forcing formed on the device).  Prints one JSON
+line per configuration and writes them all to --out.
 
     python tools/drop_in_timing.py --ncol 1048576 --steps 20 --out gpurun_out/dropin.json
 """
@@ -33,8 +35,9 @@ def main():
     ap.add_argument("--ncol", type=int, default=1 << 20)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--out", default=None)
-    ap.add_argument("--configs", default="1:6:1,1:6:2,1:6:4,1:6:8,1:1:4,0:6:4",
-                    help="pinned:out_every:chunks,...")
+    ap.add_argument("--configs", default="1:6:1,1:6:2,1:6:4,1:6:8,1:1:4,0:6:4,1:6:4:1,1:1:4:1,"
+                                          "1:6:8:1",
+                    help="pinned:out_every:chunks[:ldasin],...")
     a = ap.parse_args()
     exe = os.path.join(ROOT, "tests", "lib", "engine_drop_in")
     tbl = os.path.join(ROOT, "oracle", "_ref", "tbl")
@@ -55,10 +58,10 @@ def main():
                       frc.astype(np.float32)):
                 f.write(np.ascontiguousarray(x).tobytes())
         for cfg in a.configs.split(","):
-            pinned, oe, chunks = (int(v) for v in cfg.split(":"))
+            pinned, oe, chunks, ldasin = (tuple(int(v) for v in cfg.split(":")) + (0,))[:4]
             fout = os.path.join(td, "t.txt")
             r = subprocess.run([exe, "time", tbl, fin, fout, str(a.ncol), str(a.steps), str(oe),
-                                str(pinned), str(chunks)], capture_output=True, text=True,
+                                str(pinned), str(chunks), str(ldasin)], capture_output=True, text=True,
                                timeout=300)
             if r.returncode != 0:
                 print(r.stdout + r.stderr, file=sys.stderr)
@@ -68,7 +71,7 @@ def main():
                  "pinned": bool(int(v[3])), "ms_per_noahmp_run": float(v[4]),
                  "ms_host_forcing_fill": float(v[5]), "column_steps_per_s": float(v[6]),
                  "pcie_bytes_up_per_step": float(v[7]), "pcie_bytes_down_per_step": float(v[8]),
-                 "chunks": int(v[9])}
+                 "chunks": int(v[9]), "forcing_upload": "ldasin block" if int(v[10]) else "12 fields"}
             d["pcie_gb_per_s"] = (d["pcie_bytes_up_per_step"] + d["pcie_bytes_down_per_step"]) \
                 / (d["ms_per_noahmp_run"] * 1e-3) / 1e9
             print(json.dumps(d), flush=True)
