@@ -20,8 +20,8 @@
  *                             stops after the namelist): many steps, one launch
  * nmp_sflx_columns,           noahmp_sflx itself, argument for argument, on n host records
  *   nmp_sflx_column                                         core/module_noahmp_func.f90:66-476
- * nmp_forcing_from_ldasin     the forcing arguments of noahmp_sflx (:72-74) from the LDASIN
- *                             variables the namelist's input files carry (run/case.nml:6-7)
+ * nmp_forcing_from_ldasin,    the forcing arguments of noahmp_sflx (:72-74) from the LDASIN
+ *   nmp_forcing_from_ldasin_geo  variables the namelist's input files carry (run/case.nml:6-7)
  * nmp_frh2o, nmp_frh2o_host   frh2o (public routine)        core/module_noahmp_func.f90:4494-4598
  * nmp_calhum, nmp_calhum_host calhum (public by default)     core/module_noahmp_func.f90:3958-3984
  * nmp_state_from_aos          layout bridge from noahmp_state_t records
@@ -63,7 +63,7 @@
 extern "C" {
 #endif
 
-#define NMP_ABI_VERSION 7
+#define NMP_ABI_VERSION 8
 
 /* ---- dimensions (core/module_noahmp_global.f90:9-13) -------------------- */
 #define NMP_NSOIL 4
@@ -328,6 +328,19 @@ int nmp_forcing_synth(nmp_engine* eng, int64_t ncol, int64_t ld, const void* cli
  * array themselves and skip this call. */
 int nmp_forcing_from_ldasin(nmp_engine* eng, int64_t ncol, int64_t ld, const float* ldasin,
                             void* forcing, void* stream);
+
+/* As nmp_forcing_from_ldasin, with COSZ formed on the device instead of read
+ * from the block (its NMP_L_COSZ row is not read): geo is (3, ld) double per
+ * column -- sin(lat), cos(lat), lon (radians) -- and the step's solar terms
+ * come from the host (sin_decl, cos_decl of the declination; ha0 = 2 pi x the
+ * UTC fraction of the day).  COSZ = sin_lat sin_decl + (cos_lat cos_decl)
+ * cos((ha0 + lon) - pi) in double, rounded once to fp32: the offline driver's
+ * host expression (noahmp-1_amd/timeman.py cosz) in its operation order, with
+ * the device's double cosine.  A host then uploads an LDASIN file's 8
+ * variables once per input interval and nothing on the steps in between. */
+int nmp_forcing_from_ldasin_geo(nmp_engine* eng, int64_t ncol, int64_t ld, const float* ldasin,
+                                const double* geo, double sin_decl, double cos_decl, double ha0,
+                                void* forcing, void* stream);
 
 int nmp_run(nmp_engine* eng, int64_t ncol, int64_t ld, const float zsoil[4], float dt,
             float julian0, int32_t yearlen, int32_t nsteps, void* state, int32_t* isnow,

@@ -388,8 +388,21 @@ int nmp_forcing_from_ldasin(nmp_engine* eng, int64_t ncol, int64_t ld, const flo
   if (ncol == 0) return NMP_OK;
   if (!ldasin || !forcing) return NMP_E_ARG;
   if (ensure_device(eng->device) != NMP_OK) return NMP_E_DEVICE;
-  return nmp::launch_forcing_ldasin(eng->precision, ncol, ld, ldasin, forcing,
-                                    static_cast<hipStream_t>(stream)) == hipSuccess
+  return nmp::launch_forcing_ldasin(eng->precision, ncol, ld, ldasin, nullptr, 0.0, 0.0, 0.0,
+                                    forcing, static_cast<hipStream_t>(stream)) == hipSuccess
+             ? NMP_OK
+             : NMP_E_DEVICE;
+}
+
+int nmp_forcing_from_ldasin_geo(nmp_engine* eng, int64_t ncol, int64_t ld, const float* ldasin,
+                                const double* geo, double sin_decl, double cos_decl, double ha0,
+                                void* forcing, void* stream) {
+  if (!eng || ncol < 0 || ld < ncol || ld >= kMaxColumns) return NMP_E_ARG;
+  if (ncol == 0) return NMP_OK;
+  if (!ldasin || !geo || !forcing) return NMP_E_ARG;
+  if (ensure_device(eng->device) != NMP_OK) return NMP_E_DEVICE;
+  return nmp::launch_forcing_ldasin(eng->precision, ncol, ld, ldasin, geo, sin_decl, cos_decl, ha0,
+                                    forcing, static_cast<hipStream_t>(stream)) == hipSuccess
              ? NMP_OK
              : NMP_E_DEVICE;
 }

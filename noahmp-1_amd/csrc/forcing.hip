@@ -118,14 +118,32 @@ hipError_t launch_forcing_synth(int precision, int64_t ncol, int64_t ld, const v
 // as one IEEE double product of the fp32 pressure rounded once to fp32, every
 // field then widened to the engine precision (the host's fp32 array uploaded
 // into a T buffer).
-template <class T>
+//
+// GEO (nmp_forcing_from_ldasin_geo): COSZ is not read from the block but
+// formed per column from its latitude factors and longitude (geo, (3, ld)
+// double: sin lat, cos lat, lon) and the step's solar terms, with
+// timeman.cosz's expression and operation order in double --
+// sin_lat sin_decl + (cos_lat cos_decl) cos((ha0 + lon) - pi) -- rounded once
+// to fp32.  The block's 8 file variables then stay resident on the device for
+// every step of their input interval: nothing is uploaded between files.
+template <class T, bool GEO>
 __global__ __launch_bounds__(256) void forcing_ldasin_kernel(int64_t ncol, int64_t ld,
                                                              const float* __restrict__ in,
-                                                             T* __restrict__ out) {
+                                                             const double* __restrict__ geo,
+                                                             double sin_decl, double cos_decl,
+                                                             double ha0, T* __restrict__ out) {
   const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= ncol) return;
   const float* i = in + c;
   const float psfc = i[NMP_L_PSFC * ld];
+  float cosz;
+  if constexpr (GEO) {
+    const double* g = geo + c;
+    const double ha = (ha0 + g[2 * ld]) - 3.141592653589793;
+    cosz = (float)(g[0] * sin_decl + (g[ld] * cos_decl) * cos(ha));
+  } else {
+    cosz = i[NMP_L_COSZ * ld];
+  }
   T* o = out + c;
   o[NMP_A_SFCTMP * ld] = (T)i[NMP_L_T2D * ld];
   o[NMP_A_SFCPRS * ld] = (T)psfc;
@@ -136,21 +154,34 @@ __global__ __launch_bounds__(256) void forcing_ldasin_kernel(int64_t ncol, int64
   o[NMP_A_SOLDN * ld] = (T)i[NMP_L_SWDOWN * ld];
   o[NMP_A_LWDN * ld] = (T)i[NMP_L_LWDOWN * ld];
   o[NMP_A_PRCP * ld] = (T)i[NMP_L_RAINRATE * ld];
-  o[NMP_A_COSZ * ld] = (T)i[NMP_L_COSZ * ld];
+  o[NMP_A_COSZ * ld] = (T)cosz;
   o[NMP_A_CO2AIR * ld] = (T)(float)(395.0e-6 * (double)psfc);
   o[NMP_A_O2AIR * ld] = (T)(float)(0.209 * (double)psfc);
 }
 
+template <class T>
+static void launch_ldasin_t(int64_t grid, int64_t ncol, int64_t ld, const float* in,
+                            const double* geo, double sd, double cd, double ha0, T* out,
+                            hipStream_t stream) {
+  if (geo)
+    hipLaunchKernelGGL((forcing_ldasin_kernel<T, true>), dim3((unsigned)grid), dim3(256), 0,
+                       stream, ncol, ld, in, geo, sd, cd, ha0, out);
+  else
+    hipLaunchKernelGGL((forcing_ldasin_kernel<T, false>), dim3((unsigned)grid), dim3(256), 0,
+                       stream, ncol, ld, in, geo, sd, cd, ha0, out);
+}
+
 hipError_t launch_forcing_ldasin(int precision, int64_t ncol, int64_t ld, const float* in,
+                                 const double* geo, double sin_decl, double cos_decl, double ha0,
                                  void* out, hipStream_t stream) {
   const int64_t grid = (ncol + 255) / 256;
   if (grid == 0) return hipSuccess;
   if (precision == 4)
-    hipLaunchKernelGGL(forcing_ldasin_kernel<float>, dim3((unsigned)grid), dim3(256), 0, stream,
-                       ncol, ld, in, static_cast<float*>(out));
+    launch_ldasin_t(grid, ncol, ld, in, geo, sin_decl, cos_decl, ha0, static_cast<float*>(out),
+                    stream);
   else
-    hipLaunchKernelGGL(forcing_ldasin_kernel<double>, dim3((unsigned)grid), dim3(256), 0, stream,
-                       ncol, ld, in, static_cast<double*>(out));
+    launch_ldasin_t(grid, ncol, ld, in, geo, sin_decl, cos_decl, ha0, static_cast<double*>(out),
+                    stream);
   return hipGetLastError();
 }
 

@@ -61,8 +61,10 @@ hipError_t launch_forcing_synth(int precision, int64_t ncol, int64_t ld, const v
                                 double julian, int32_t yearlen, uint64_t seed, int64_t step,
                                 int64_t first_col, void* out, hipStream_t stream);
 
-// csrc/forcing.hip: the 12 forcing fields from the LDASIN block (fp32)
+// csrc/forcing.hip: the 12 forcing fields from the LDASIN block (fp32); with
+// geo (not null) COSZ formed on the device from the columns' geometry
 hipError_t launch_forcing_ldasin(int precision, int64_t ncol, int64_t ld, const float* in,
+                                 const double* geo, double sin_decl, double cos_decl, double ha0,
                                  void* out, hipStream_t stream);
 
 // csrc/routines.hip: the reference's public routines frh2o / calhum over n

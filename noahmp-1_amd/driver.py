@@ -30,11 +30,15 @@ allowed), which writes them for the whole grid.
 
 Forcing reaches the GPU through `ForcingUpload`: pinned, double-buffered
 host buffers copied on a copy stream, so the host builds step t+1's forcing
-while the GPU steps t.  From LDASIN files the upload is the files' own
-variables plus COSZ (ncio.LdasinForcing.raw, 36 B per column in fp32), and
-the engine forms the 12 forcing fields on each range's stream right before
-its launch (nmp_forcing_from_ldasin); the 12-field host form (48 B per
-column, 96 in fp64) remains for providers that supply all of them.
+while the GPU steps t.  From LDASIN files (cosz="device", the default) the
+upload is a file's 8 variables, once per input interval (ncio.LdasinForcing
+.block, 32 B per column per file), which stay resident while the engine forms
+the 12 forcing fields, COSZ included, on each range's stream right before its
+launch (nmp_forcing_from_ldasin_geo): no host work and no upload on the steps
+between files.  cosz="host" uploads the variables plus the host's COSZ every
+step (ncio.LdasinForcing.raw, 36 B per column, nmp_forcing_from_ldasin); the
+12-field host form (48 B per column, 96 in fp64) remains for providers that
+supply all of them.
 
 `phase_s` accumulates the host time of the loop's parts (forcing provider,
 upload enqueue, launch enqueue, output), for the offline-driver timing
@@ -158,12 +162,18 @@ class OfflineDriver:
     def __init__(self, cfg: Config, cols: cases.ColumnSet, device: int = 0,
                  params: Params | None = None, forcing=None, precision: int = 4,
                  math: str = "ref", zsoil=cases.CASE_NML_ZSOIL, write: bool = True,
-                 streams: int = 2, grid: ncio.Grid | None = None, ldasin_upload: bool = True):
+                 streams: int = 2, grid: ncio.Grid | None = None, ldasin_upload: bool = True,
+                 cosz: str = "device"):
         """cols: this rank's columns (all of them on a single rank); under an
         initialised process group they must be the rank's shard_range block of
         the global column set.  ldasin_upload: with a provider that has
         `raw` (LDASIN files), upload the files' variables and form the forcing
-        on the device (False: the 12-field host form, for comparison)."""
+        on the device (False: the 12-field host form, for comparison).
+        cosz: with ldasin_upload, "device" forms COSZ on the device from the
+        columns' geometry (the files' variables then go up once per input
+        interval), "host" computes it on the host and uploads it every step."""
+        if cosz not in ("device", "host"):
+            raise ValueError(f"cosz must be 'device' or 'host', not {cosz!r}")
         self.cfg = cfg
         self.grid = grid
         self.engine = Engine(params or Params.builtin(), cfg.engine_options(), device, precision,
@@ -202,6 +212,9 @@ class OfflineDriver:
                                             nfield=L.NLDASIN)
             self.raw_fbuf = torch.empty((2, L.NFORCING, self.cs.ncol), dtype=self.dtype,
                                         device=self.dev)
+        self.geo, self._raw_t, self._raw = None, None, None
+        if self.raw_upload is not None and cosz == "device":
+            self.geo = torch.as_tensor(self.forcing.geo(), device=self.dev).contiguous()
         self.phase_s = defaultdict(float)
         self.gather = None
         if dist.is_initialized():
@@ -310,10 +323,24 @@ class OfflineDriver:
                 # the LDASIN block straight into a pinned buffer and up; each
                 # range forms its 12 fields on its own stream before its launch
                 step_k, t_k = self.step_index, t0
-                raw = self.raw_upload.put(fill=lambda h: self.forcing.raw(step_k, t_k, out=h))
+                geo = solar = None
+                if self.geo is not None:
+                    # the file's variables go up once per input interval and
+                    # stay resident; COSZ is formed on the device every step
+                    ti = self.forcing.input_time(t0)
+                    if ti != self._raw_t:
+                        self._raw = self.raw_upload.put(
+                            fill=lambda h: self.forcing.block(t_k, out=h))
+                        self._raw_t = ti
+                    raw = self._raw
+                    if not self.forcing.file_cosz(t0):
+                        geo = self.geo
+                        solar = timeman.solar_terms(timeman.julian(t0), timeman.yearlen(t0.year))
+                else:
+                    raw = self.raw_upload.put(fill=lambda h: self.forcing.raw(step_k, t_k, out=h))
                 f = self.raw_fbuf[self.step_index % 2]
                 pre = lambda st, rng: self.engine.forcing_from_ldasin(  # noqa: E731
-                    raw, f, stream=st, cols=rng)
+                    raw, f, stream=st, cols=rng, geo=geo, solar=solar)
                 after, upload = (cur, self.raw_upload.stream), self.raw_upload
             elif self.dev_forcing is not None:
                 clim, fbuf = self.dev_forcing

@@ -219,23 +219,36 @@ class Engine:
                                                C.c_void_p(s.cuda_stream)), "nmp_forcing_synth")
 
     def forcing_from_ldasin(self, ldasin: torch.Tensor, out: torch.Tensor, stream=None,
-                            cols: tuple[int, int] | None = None):
+                            cols: tuple[int, int] | None = None, geo: torch.Tensor | None = None,
+                            solar: tuple[float, float, float] | None = None):
         """nmp_forcing_from_ldasin: the 12 forcing fields of one step into out
         (NFORCING, n), engine precision, from the (NLDASIN, n) fp32 LDASIN
         block (layout.LDASIN); SFCPRS, CO2AIR and O2AIR formed on the device
-        from PSFC.  cols=(lo, hi) converts only those columns."""
+        from PSFC.  cols=(lo, hi) converts only those columns.
+
+        geo, solar (nmp_forcing_from_ldasin_geo): COSZ formed on the device from
+        geo = (3, n) float64 (sin lat, cos lat, lon; ncio.LdasinForcing.geo)
+        and solar = timeman.solar_terms(julian, yearlen) instead of read from
+        the block's COSZ row."""
         n = int(ldasin.shape[1])
         lo, hi = (0, n) if cols is None else (int(cols[0]), int(cols[1]))
         assert 0 <= lo <= hi <= n
         assert ldasin.shape == (L.NLDASIN, n) and ldasin.dtype == torch.float32
         assert out.shape == (L.NFORCING, n) and out.dtype == self.dtype
         assert ldasin.is_contiguous() and out.is_contiguous()
-        for t in (ldasin, out):
+        for t in (ldasin, out) + ((geo,) if geo is not None else ()):
             assert t.device.type == "cuda" and t.device.index == self.device
         s = stream if stream is not None else torch.cuda.current_stream(self.device)
-        _lib.check(self._lib.nmp_forcing_from_ldasin(self._h, hi - lo, n, _ptr(ldasin, lo),
-                                                     _ptr(out, lo), C.c_void_p(s.cuda_stream)),
-                   "nmp_forcing_from_ldasin")
+        if geo is None:
+            _lib.check(self._lib.nmp_forcing_from_ldasin(self._h, hi - lo, n, _ptr(ldasin, lo),
+                                                         _ptr(out, lo), C.c_void_p(s.cuda_stream)),
+                       "nmp_forcing_from_ldasin")
+            return
+        assert geo.shape == (3, n) and geo.dtype == torch.float64 and geo.is_contiguous()
+        sd, cd, ha0 = (float(v) for v in solar)
+        _lib.check(self._lib.nmp_forcing_from_ldasin_geo(
+            self._h, hi - lo, n, _ptr(ldasin, lo), _ptr(geo, lo), sd, cd, ha0, _ptr(out, lo),
+            C.c_void_p(s.cuda_stream)), "nmp_forcing_from_ldasin_geo")
 
     # ---- the reference's other public routines (nmp_frh2o / nmp_calhum) ------
     def frh2o(self, sltyp, tkelv, smc, sh2o, status=None, stream=None):

@@ -386,6 +386,35 @@ class LdasinForcing:
         self._chunks(fill)
         return r
 
+    def block(self, t: datetime.datetime, out: np.ndarray | None = None):
+        """The LDASIN block of the input interval holding t without the
+        per-step COSZ: the 8 file variables (and the file's own COSZ when it
+        carries one; else that row is left as it is), for a host that uploads
+        them once per input interval and forms COSZ on the device
+        (nmp_forcing_from_ldasin_geo with `geo`).  None when the file carries
+        CO2AIR / O2AIR of its own."""
+        fl = self.fields(t)
+        if "CO2AIR" in fl or "O2AIR" in fl:
+            return None
+        r = np.empty((L.NLDASIN, self.lat.shape[0]), np.float32) if out is None else out
+        rows = [(i, v) for i, v in enumerate(L.LDASIN) if v != "COSZ" or "COSZ" in fl]
+
+        def fill(c):
+            for i, var in rows:
+                r[i, c] = fl[var][c]
+        self._chunks(fill)
+        return r
+
+    def file_cosz(self, t: datetime.datetime) -> bool:
+        """The input file of t carries COSZ (then it, not the solar geometry, is the step's)."""
+        return "COSZ" in self.fields(t)
+
+    def geo(self) -> np.ndarray:
+        """(3, n) float64 per column: sin lat, cos lat, lon (radians) -- the
+        column factors of timeman.cosz, the same values it evaluates."""
+        return np.stack([self._sincos_lat[0], self._sincos_lat[1],
+                         np.asarray(self.lon, np.float64)])
+
 
 # ---- LDASOUT ----------------------------------------------------------------------
 def write_ldasout(path: str, grid: Grid, diag: np.ndarray, t: datetime.datetime):

@@ -30,14 +30,23 @@ def step_times(begin: _dt.datetime, end: _dt.datetime, dt_seconds: float):
     return [begin + _dt.timedelta(seconds=dt_seconds * (i + 1)) for i in range(n)]
 
 
-def cosz(lat_rad, lon_rad, jul: float, ylen: int, sincos_lat=None):
-    """Cosine of the solar zenith angle (simple declination + hour angle).
-    sincos_lat: (np.sin(lat), np.cos(lat)) precomputed by a caller that
-    evaluates many steps of the same columns (the same values)."""
+def solar_terms(jul: float, ylen: int):
+    """The step's column-independent factors of cosz: (sin decl, cos decl,
+    ha0), ha0 = 2 pi x the UTC fraction of the day.  The device form of cosz
+    (nmp_forcing_from_ldasin_geo) takes these from the host."""
     decl = 0.409 * math.sin(2.0 * math.pi * (jul - 80.0) / ylen)
     hour_utc = (jul - math.floor(jul)) * 24.0
-    ha = 2.0 * math.pi * (hour_utc / 24.0) + np.asarray(lon_rad) - math.pi
+    return math.sin(decl), math.cos(decl), 2.0 * math.pi * (hour_utc / 24.0)
+
+
+def cosz(lat_rad, lon_rad, jul: float, ylen: int, sincos_lat=None):
+    """Cosine of the solar zenith angle (simple declination + hour angle):
+    sin lat sin decl + (cos lat cos decl) cos((ha0 + lon) - pi), in double.
+    sincos_lat: (np.sin(lat), np.cos(lat)) precomputed by a caller that
+    evaluates many steps of the same columns (the same values)."""
+    sd, cd, ha0 = solar_terms(jul, ylen)
+    ha = ha0 + np.asarray(lon_rad) - math.pi
     if sincos_lat is None:
         lat = np.asarray(lat_rad)
         sincos_lat = (np.sin(lat), np.cos(lat))
-    return sincos_lat[0] * math.sin(decl) + sincos_lat[1] * math.cos(decl) * np.cos(ha)
+    return sincos_lat[0] * sd + sincos_lat[1] * cd * np.cos(ha)

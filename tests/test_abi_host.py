@@ -85,7 +85,7 @@ def test_params_struct_size():
 
 
 def test_abi_version_and_errors(engine_lib):
-    assert engine_lib.nmp_abi_version() == 7
+    assert engine_lib.nmp_abi_version() == 8
     for code in (0, -1, -2, -3, -4, -5, -6, -99):
         assert engine_lib.nmp_strerror(code)
     assert b"year boundary" in engine_lib.nmp_strerror(-6)

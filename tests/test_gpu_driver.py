@@ -109,11 +109,16 @@ def test_driver_from_netcdf_files(engine_lib, tmp_path):
 @pytest.mark.parametrize("precision", [4, 8])
 def test_driver_ldasin_block_equals_host_fields(engine_lib, tmp_path, precision):
     """Standard HRLDAS files (the 8 LDASIN variables only; COSZ from the grid,
-    CO2AIR / O2AIR from PSFC): the driver uploads the LDASIN block and the
-    engine forms the 12 fields on each range's stream (nmp_forcing_from_ldasin),
-    or builds the 12 fields on the host (ldasin_upload=False).  Both runs give
-    the same state, ISNOW and LDASOUT files bit for bit, in fp32 and fp64,
-    from two host threads or one."""
+    CO2AIR / O2AIR from PSFC): the driver uploads the LDASIN block with the
+    host's COSZ every step and the engine forms the 12 fields on each range's
+    stream (nmp_forcing_from_ldasin, cosz="host"), or uploads each file's
+    variables once per input interval and forms COSZ on the device as well
+    (nmp_forcing_from_ldasin_geo, cosz="device": 24 uploads for 96 steps), or
+    builds the 12 fields on the host (ldasin_upload=False).  All three runs
+    give the same state, ISNOW and LDASOUT files bit for bit, in fp32 and
+    fp64, from two host threads or one.  (The device COSZ equals the host's
+    on every one of these 3,072 column-steps -- checked first, so a rounding
+    difference of the two double cosines would be named as such.)"""
     from noahmp_amd import ncio
     from test_config import write_case
     from test_ncio import grid_for
@@ -134,23 +139,46 @@ def test_driver_ldasin_block_equals_host_fields(engine_lib, tmp_path, precision)
         ncio.write_ldasin(ncio.ldasin_path(str(indir), t), grid, g["forcing"][k], t, extras=False)
         t = t + cfg.input_interval
     runs = []
-    for ldasin, threads in ((False, 1), (True, 2)):
-        cfg.outdir = str(tmp_path / f"out_{int(ldasin)}")
+    for ldasin, threads, cz in ((False, 1, "host"), (True, 2, "host"), (True, 2, "device")):
+        cfg.outdir = str(tmp_path / f"out_{int(ldasin)}_{cz}")
         drv = driver.OfflineDriver.from_files(cfg, precision=precision, ldasin_upload=ldasin,
-                                              host_threads=threads).run()
+                                              host_threads=threads, cosz=cz)
+        if cz == "device":
+            _check_device_cosz_equals_host(drv, cfg, 96)
+        drv.run()
         assert drv.step_index == 96
-        assert (drv.raw_upload is not None and drv.raw_upload.count == 96) == ldasin
+        uploads = 0 if not ldasin else (96 if cz == "host" else 24)
+        assert (drv.raw_upload.count if drv.raw_upload is not None else 0) == uploads
         assert drv.upload.count == (0 if ldasin else 96)
         outs = [ncio.read_ldasout(f, grid) for f in sorted(
             glob.glob(os.path.join(cfg.outdir, "*.LDASOUT_DOMAIN1")))]
         assert len(outs) == 8
         runs.append((drv.cs.state.cpu().numpy(), drv.cs.isnow.cpu().numpy(), outs))
         drv.engine.close()
-    (s0, i0, o0), (s1, i1, o1) = runs
-    assert bit_equal(s1, s0).all() and np.array_equal(i1, i0)
-    for a, b in zip(o1, o0):
-        assert bit_equal(a, b).all()
-    assert np.isfinite(s1[L.s("STC")]).all()
+    s0, i0, o0 = runs[0]
+    for s1, i1, o1 in runs[1:]:
+        assert bit_equal(s1, s0).all() and np.array_equal(i1, i0)
+        for a, b in zip(o1, o0):
+            assert bit_equal(a, b).all()
+    assert np.isfinite(s0[L.s("STC")]).all()
+
+
+def _check_device_cosz_equals_host(drv, cfg, nsteps):
+    """The COSZ nmp_forcing_from_ldasin_geo forms for each of the run's steps
+    equals the host reader's (timeman.cosz rounded to fp32) on every column."""
+    from noahmp_amd import timeman
+    fr = drv.forcing
+    geo = torch.as_tensor(fr.geo(), device=drv.dev)
+    blk = torch.zeros((L.NLDASIN, drv.cs.ncol), dtype=torch.float32, device=drv.dev)
+    out = torch.empty((L.NFORCING, drv.cs.ncol), dtype=drv.dtype, device=drv.dev)
+    t = cfg.begdatetime
+    for k in range(nsteps):
+        jul, yl = timeman.julian(t), timeman.yearlen(t.year)
+        drv.engine.forcing_from_ldasin(blk, out, geo=geo, solar=timeman.solar_terms(jul, yl))
+        got = out[L.FORCING.index("COSZ")].cpu().numpy().astype(np.float32)
+        want = timeman.cosz(fr.lat, fr.lon, jul, yl).astype(np.float32)
+        assert bit_equal(got, want).all(), f"step {k}: device COSZ differs from the host's"
+        t = t + cfg.timestep
 
 
 def test_offline_cli_runs_a_netcdf_case(engine_lib, tmp_path):

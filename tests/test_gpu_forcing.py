@@ -115,3 +115,56 @@ def test_forcing_from_ldasin_equals_host_reader(engine_lib, precision):
                           want.view(np.int32 if precision == 4 else np.int64))
     assert torch.equal(a.view(iv), b.view(iv))
     eng.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("precision", [4, 8])
+def test_forcing_from_ldasin_geo_device_cosz(engine_lib, precision):
+    """nmp_forcing_from_ldasin_geo: COSZ formed on the device from the columns'
+    (sin lat, cos lat, lon) and the step's solar terms, in timeman.cosz's
+    expression and order, rounded to fp32.  Over 1,000,003 columns spread over
+    the globe and 8 times of day through a year, it equals the host's
+    (numpy double cosine) on at least 99.999 % of the column-steps and is never
+    more than 1 fp32 ulp away; the block's COSZ row is not read; the other 11
+    fields are nmp_forcing_from_ldasin's, bit for bit; column ranges give the
+    one-launch result."""
+    from noahmp_amd import timeman
+    from noahmp_amd.engine import Engine
+    from noahmp_amd.params import Params
+    dt = torch.float32 if precision == 4 else torch.float64
+    n = 1_000_003
+    rng = np.random.default_rng(11)
+    lat = np.radians(rng.uniform(-89.9, 89.9, n))
+    lon = np.radians(rng.uniform(-180.0, 180.0, n))
+    geo = torch.as_tensor(np.stack([np.sin(lat), np.cos(lat), lon]), device=DEV)
+    raw = rng.uniform(1.0, 2.0, (L.NLDASIN, n)).astype(np.float32)
+    raw[L.LDASIN.index("PSFC")] *= 5.0e4
+    r = torch.as_tensor(raw, device=DEV)
+    eng = Engine(Params.builtin(), L.CASE_NML_OPTIONS, device=0, precision=precision)
+    a = torch.zeros((L.NFORCING, n), dtype=dt, device=DEV)
+    b = torch.full_like(a, float("nan"))
+    plain = torch.zeros_like(a)
+    eng.forcing_from_ldasin(r, plain)
+    ci = L.FORCING.index("COSZ")
+    mism, total = 0, 0
+    for jul in (1.0, 45.3125, 100.5, 172.75, 200.0625, 266.875, 300.4375, 365.9583):
+        solar = timeman.solar_terms(jul, 366)
+        eng.forcing_from_ldasin(r, a, geo=geo, solar=solar)
+        for lo, hi in ((0, 65_537), (65_537, 700_000), (700_000, n)):
+            eng.forcing_from_ldasin(r, b, cols=(lo, hi), geo=geo, solar=solar)
+        torch.cuda.synchronize()
+        iv = torch.int32 if precision == 4 else torch.int64
+        assert torch.equal(a.view(iv), b.view(iv))
+        keep = [i for i in range(L.NFORCING) if i != ci]
+        assert torch.equal(a[keep].view(iv), plain[keep].view(iv))
+        got = a[ci].cpu().numpy().astype(np.float32)
+        want = timeman.cosz(lat, lon, jul, 366).astype(np.float32)
+        ulps = np.abs(got.view(np.int32).astype(np.int64) - want.view(np.int32).astype(np.int64))
+        # (same-sign values: the int distance is the ulp distance; |COSZ| <= 1)
+        same = np.sign(got) == np.sign(want)
+        assert (ulps[same] <= 1).all() and (got[~same] == want[~same]).all()
+        mism += int((ulps != 0).sum())
+        total += n
+    print(f"device COSZ: {mism} of {total} column-steps differ from numpy's by 1 fp32 ulp")
+    assert mism <= 1e-5 * total
+    eng.close()

@@ -95,6 +95,19 @@ def test_ldasin_round_trip_and_derived_fields(tmp_path, ref_params):
          "CO2AIR": np.float32(395.0e-6 * R["PSFC"].astype(np.float64)),
          "O2AIR": np.float32(0.209 * R["PSFC"].astype(np.float64))}
     assert np.array_equal(bits(np.stack([x[k] for k in L.FORCING])), bits(g))
+    # the once-per-interval block (device COSZ): the 8 file variables as in
+    # raw, the COSZ row left alone (the file has none), and the geometry whose
+    # COSZ expression, restated from solar_terms, is timeman.cosz's bit for bit
+    blk = np.full((L.NLDASIN, 32), -7.0, np.float32)
+    assert prov2.block(t, out=blk) is blk and not prov2.file_cosz(t)
+    ci = L.LDASIN.index("COSZ")
+    assert np.array_equal(bits(np.delete(blk, ci, 0)), bits(np.delete(raw, ci, 0)))
+    assert (blk[ci] == -7.0).all()
+    geo = prov2.geo()
+    assert geo.dtype == np.float64 and geo.shape == (3, 32)
+    sd, cd, ha0 = timeman.solar_terms(timeman.julian(t), 366)
+    cz_geo = geo[0] * sd + (geo[1] * cd) * np.cos((ha0 + geo[2]) - np.pi)
+    assert np.array_equal(bits(cz_geo.astype(np.float32)), bits(cz))
     # a file with its own CO2AIR / O2AIR has no block form
     ncio.write_ldasin(ncio.ldasin_path(str(d), T0), grid, f, T0, extras=("CO2AIR",))
     assert ncio.LdasinForcing(str(d), grid, T0, datetime.timedelta(hours=1)).raw(0, T0) is None

@@ -7,8 +7,10 @@ LDASIN files without CO2AIR / O2AIR, the standard HRLDAS set) for
 examples/offline_case.nml's day (96 steps of 900 s, output every 3 hours),
 then runs `OfflineDriver.from_files` over it in each upload mode and
 precision: the 12 forcing fields built on the host and uploaded (48 B per
-column per step in fp32, 96 in fp64), and the LDASIN block (the files' 8
-variables + COSZ, fp32, 36 B) expanded on the device (nmp_forcing_from_ldasin).
+column per step in fp32, 96 in fp64), the LDASIN block (the files' 8
+variables + COSZ, fp32, 36 B) expanded on the device (nmp_forcing_from_ldasin),
+and that block uploaded once per input file with COSZ formed on the device
+(cosz="device", nmp_forcing_from_ldasin_geo: no upload between files).
 After 4 warm-up steps the remaining steps are timed, wall clock between two
 synchronizes, with the driver's own per-phase host times (`phase_s`: LDASIN
 file reads, forcing build + upload enqueue, launch enqueue, output gather +
@@ -44,16 +46,17 @@ def write_namelist(d: str) -> str:
     return p
 
 
-def time_driver(cfg, precision, ldasin, warm, steps, threads):
+def time_driver(cfg, precision, ldasin, warm, steps, threads, cosz="host"):
     import torch
     t0 = time.perf_counter()
     drv = driver.OfflineDriver.from_files(cfg, precision=precision, ldasin_upload=ldasin,
-                                          host_threads=threads)
+                                          host_threads=threads, cosz=cosz)
     setup = time.perf_counter() - t0
     drv.run(nsteps=warm)
     torch.cuda.synchronize()
     drv.phase_s.clear()
     n_written = len(drv.written)
+    up0 = (drv.raw_upload or drv.upload).count
     t0 = time.perf_counter()
     drv.run(nsteps=steps)
     torch.cuda.synchronize()
@@ -61,11 +64,14 @@ def time_driver(cfg, precision, ldasin, warm, steps, threads):
     n = drv.cs.ncol
     outs = len(drv.written) - n_written
     bpc = 4 * L.NLDASIN if drv.raw_upload is not None else precision * L.NFORCING
-    res = {"precision": precision, "upload": "ldasin block" if drv.raw_upload is not None
-           else "12 fields", "host_threads": threads, "ncol": n, "steps": steps, "output_steps": outs,
+    puts = (drv.raw_upload or drv.upload).count - up0
+    kind = "12 fields" if drv.raw_upload is None else (
+        "ldasin block + device cosz" if drv.geo is not None else "ldasin block")
+    res = {"precision": precision, "upload": kind, "host_threads": threads, "ncol": n,
+           "steps": steps, "output_steps": outs, "uploads": puts,
            "wall_s": el, "ms_per_step": el * 1e3 / steps, "colsteps_per_s": n * steps / el,
            "phase_ms_per_step": {k: v * 1e3 / steps for k, v in drv.phase_s.items()},
-           "pcie_up_bytes_per_step": bpc * n,
+           "pcie_up_bytes_per_step": bpc * n * puts / steps,
            "pcie_down_bytes_per_output_step": L.NDIAG_OUT * precision * n,
            "setup_s": setup,
            "status_nonzero_cols": int((drv.cs.status != 0).sum().item())}
@@ -122,11 +128,17 @@ def main():
         states = []
         # round 5's path (12 fields, one host thread), the threaded host build,
         # and the LDASIN block expanded on the device
-        for ldasin, threads in ((False, 1), (False, a.threads), (True, a.threads)):
-            r, st, drv = time_driver(cfg, prec, ldasin, a.warm, a.steps, threads)
+        # and the block once per file with COSZ formed on the device
+        for ldasin, threads, cz in ((False, 1, "host"), (False, a.threads, "host"),
+                                    (True, a.threads, "host"), (True, a.threads, "device")):
+            r, st, drv = time_driver(cfg, prec, ldasin, a.warm, a.steps, threads, cz)
             states.append(st)
             r["state_equals_first_run"] = bool(np.array_equal(states[0].view(np.uint8),
                                                               st.view(np.uint8)))
+            if cz == "device":  # COSZ from the device's double cosine: columns apart by 1 ulp
+                iv = np.uint32 if st.dtype == np.float32 else np.uint64
+                r["state_cols_differing_from_first_run"] = int(
+                    (states[0].view(iv) != st.view(iv)).any(0).sum())
             print(json.dumps(r), flush=True)
             runs.append(r)
         e = time_engine(drv, prec, a.steps)
