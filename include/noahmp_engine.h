@@ -21,7 +21,8 @@
  * nmp_sflx_columns,           noahmp_sflx itself, argument for argument, on n host records
  *   nmp_sflx_column                                         core/module_noahmp_func.f90:66-476
  * nmp_forcing_from_ldasin,    the forcing arguments of noahmp_sflx (:72-74) from the LDASIN
- *   nmp_forcing_from_ldasin_geo  variables the namelist's input files carry (run/case.nml:6-7)
+ *   nmp_forcing_from_ldasin_geo, variables the namelist's input files carry (run/case.nml:6-7)
+ *   nmp_ldasin_ingest
  * nmp_frh2o, nmp_frh2o_host   frh2o (public routine)        core/module_noahmp_func.f90:4494-4598
  * nmp_calhum, nmp_calhum_host calhum (public by default)     core/module_noahmp_func.f90:3958-3984
  * nmp_state_from_aos          layout bridge from noahmp_state_t records
@@ -341,6 +342,18 @@ int nmp_forcing_from_ldasin(nmp_engine* eng, int64_t ncol, int64_t ld, const flo
 int nmp_forcing_from_ldasin_geo(nmp_engine* eng, int64_t ncol, int64_t ld, const float* ldasin,
                                 const double* geo, double sin_decl, double cos_decl, double ha0,
                                 void* forcing, void* stream);
+
+/* Rows NMP_L_T2D..NMP_L_LWDOWN of an LDASIN block (fp32, leading dimension
+ * ld, ncol columns) from the file's own bytes: grid_be holds the 8 variables
+ * in NMP_L_* order, each npts grid points of big-endian fp32 as a netCDF-3
+ * file stores them, and column c of the block takes grid point point[c]
+ * (the land-point selection and the host's column order in one index; a
+ * column whose point lies outside [0, npts) gets NaN rows).  The NMP_L_COSZ
+ * row is not written.  A host then
+ * copies each file's bytes and uploads them; byte order and gather happen
+ * here.  Device pointers, enqueued on `stream`. */
+int nmp_ldasin_ingest(nmp_engine* eng, int64_t ncol, int64_t ld, int64_t npts,
+                      const void* grid_be, const int32_t* point, float* ldasin, void* stream);
 
 int nmp_run(nmp_engine* eng, int64_t ncol, int64_t ld, const float zsoil[4], float dt,
             float julian0, int32_t yearlen, int32_t nsteps, void* state, int32_t* isnow,

@@ -394,6 +394,19 @@ int nmp_forcing_from_ldasin(nmp_engine* eng, int64_t ncol, int64_t ld, const flo
              : NMP_E_DEVICE;
 }
 
+int nmp_ldasin_ingest(nmp_engine* eng, int64_t ncol, int64_t ld, int64_t npts,
+                      const void* grid_be, const int32_t* point, float* ldasin, void* stream) {
+  if (!eng || ncol < 0 || ld < ncol || ld >= kMaxColumns || npts < 0 || npts >= kMaxColumns)
+    return NMP_E_ARG;
+  if (ncol == 0) return NMP_OK;
+  if (!grid_be || !point || !ldasin || npts == 0) return NMP_E_ARG;
+  if (ensure_device(eng->device) != NMP_OK) return NMP_E_DEVICE;
+  return nmp::launch_ldasin_ingest(ncol, ld, npts, grid_be, point, ldasin,
+                                   static_cast<hipStream_t>(stream)) == hipSuccess
+             ? NMP_OK
+             : NMP_E_DEVICE;
+}
+
 int nmp_forcing_from_ldasin_geo(nmp_engine* eng, int64_t ncol, int64_t ld, const float* ldasin,
                                 const double* geo, double sin_decl, double cos_decl, double ha0,
                                 void* forcing, void* stream) {

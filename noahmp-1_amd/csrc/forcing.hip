@@ -185,4 +185,36 @@ hipError_t launch_forcing_ldasin(int precision, int64_t ncol, int64_t ld, const 
   return hipGetLastError();
 }
 
+// An LDASIN file's 8 variables as the netCDF-3 file stores them -- each a
+// big-endian fp32 grid of npts points, in NMP_L_* order -- into the block's
+// rows NMP_L_T2D..NMP_L_LWDOWN in engine column order (nmp_ldasin_ingest):
+// column c takes grid point point[c].  The host only copies the file's bytes;
+// the land-point selection, the engine's column order and the byte order are
+// applied here, one gathered 4-byte load per variable and column.
+__global__ __launch_bounds__(256) void ldasin_ingest_kernel(int64_t ncol, int64_t ld, int64_t npts,
+                                                            const uint32_t* __restrict__ grid_be,
+                                                            const int32_t* __restrict__ point,
+                                                            float* __restrict__ block) {
+  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= ncol) return;
+  const int64_t p = point[c];
+  if (p < 0 || p >= npts) {  // outside the grid: NaN, never an out-of-bounds load
+#pragma unroll
+    for (int v = 0; v < NMP_L_COSZ; ++v) block[v * ld + c] = __int_as_float(0x7fc00000);
+    return;
+  }
+#pragma unroll
+  for (int v = 0; v < NMP_L_COSZ; ++v)
+    block[v * ld + c] = __uint_as_float(__builtin_bswap32(grid_be[v * npts + p]));
+}
+
+hipError_t launch_ldasin_ingest(int64_t ncol, int64_t ld, int64_t npts, const void* grid_be,
+                                const int32_t* point, float* block, hipStream_t stream) {
+  const int64_t grid = (ncol + 255) / 256;
+  if (grid == 0) return hipSuccess;
+  hipLaunchKernelGGL(ldasin_ingest_kernel, dim3((unsigned)grid), dim3(256), 0, stream, ncol, ld,
+                     npts, static_cast<const uint32_t*>(grid_be), point, block);
+  return hipGetLastError();
+}
+
 }  // namespace nmp

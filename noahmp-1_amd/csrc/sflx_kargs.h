@@ -66,6 +66,9 @@ hipError_t launch_forcing_synth(int precision, int64_t ncol, int64_t ld, const v
 hipError_t launch_forcing_ldasin(int precision, int64_t ncol, int64_t ld, const float* in,
                                  const double* geo, double sin_decl, double cos_decl, double ha0,
                                  void* out, hipStream_t stream);
+// csrc/forcing.hip: an LDASIN file's big-endian grids -> the block's 8 rows
+hipError_t launch_ldasin_ingest(int64_t ncol, int64_t ld, int64_t npts, const void* grid_be,
+                                const int32_t* point, float* block, hipStream_t stream);
 
 // csrc/routines.hip: the reference's public routines frh2o / calhum over n
 // elements (device pointers, engine precision; math 0 = the fp32 "ref" policy)

@@ -163,7 +163,7 @@ class OfflineDriver:
                  params: Params | None = None, forcing=None, precision: int = 4,
                  math: str = "ref", zsoil=cases.CASE_NML_ZSOIL, write: bool = True,
                  streams: int = 2, grid: ncio.Grid | None = None, ldasin_upload: bool = True,
-                 cosz: str = "device"):
+                 cosz: str = "device", ingest: bool = True):
         """cols: this rank's columns (all of them on a single rank); under an
         initialised process group they must be the rank's shard_range block of
         the global column set.  ldasin_upload: with a provider that has
@@ -171,7 +171,11 @@ class OfflineDriver:
         on the device (False: the 12-field host form, for comparison).
         cosz: with ldasin_upload, "device" forms COSZ on the device from the
         columns' geometry (the files' variables then go up once per input
-        interval), "host" computes it on the host and uploads it every step."""
+        interval), "host" computes it on the host and uploads it every step.
+        ingest: with cosz="device", upload each file's bytes as it stores them
+        (its big-endian grids, ncio.LdasinForcing.grid_raw) and select, order
+        and byte-swap this rank's columns on the device (nmp_ldasin_ingest)
+        instead of on the host (ncio.LdasinForcing.block)."""
         if cosz not in ("device", "host"):
             raise ValueError(f"cosz must be 'device' or 'host', not {cosz!r}")
         self.cfg = cfg
@@ -215,6 +219,13 @@ class OfflineDriver:
         self.geo, self._raw_t, self._raw = None, None, None
         if self.raw_upload is not None and cosz == "device":
             self.geo = torch.as_tensor(self.forcing.geo(), device=self.dev).contiguous()
+        self.ingest = None
+        if self.geo is not None and ingest and hasattr(self.forcing, "grid_raw"):
+            npts = self.forcing.grid.shape[0] * self.forcing.grid.shape[1]
+            self.ingest = ForcingUpload(npts, torch.int32, self.dev, nfield=L.NLDASIN - 1)
+            self.ingest_blk = torch.zeros((2, L.NLDASIN, self.cs.ncol), dtype=torch.float32,
+                                          device=self.dev)
+            self.point = torch.as_tensor(self.forcing.point(), device=self.dev)
         self.phase_s = defaultdict(float)
         self.gather = None
         if dist.is_initialized():
@@ -224,6 +235,12 @@ class OfflineDriver:
                                  f"shard_range block of {total} has {self.gather.n_local}")
         self.n_out = 0
         self.written = []
+        self._writer = None
+        if write and cfg.output_interval is not None and (
+                not dist.is_initialized() or dist.get_rank() == 0):
+            # the output staging buffers up front: a page-locked allocation of
+            # the whole set's fluxes costs tens of ms inside the time loop
+            self._writer_init((L.NDIAG_OUT, total))
 
     @classmethod
     def from_files(cls, cfg: Config, device: int = 0, params: Params | None = None,
@@ -316,10 +333,11 @@ class OfflineDriver:
             cur = torch.cuda.current_stream(self.dev)
             pre, after, upload = None, (cur, self.upload.stream), self.upload
             tp = time.perf_counter()
-            fl = self.forcing.fields(t0) if hasattr(self.forcing, "fields") else None
-            self.phase_s["read"] += time.perf_counter() - tp  # LDASIN files, per input time
+            # the input file's variable names (header only, once per input time)
+            info = self.forcing.variables(t0) if hasattr(self.forcing, "variables") else None
+            self.phase_s["read"] += time.perf_counter() - tp
             tp = time.perf_counter()
-            if self.raw_upload is not None and "CO2AIR" not in fl and "O2AIR" not in fl:
+            if self.raw_upload is not None and not ({"CO2AIR", "O2AIR"} & info):
                 # the LDASIN block straight into a pinned buffer and up; each
                 # range forms its 12 fields on its own stream before its launch
                 step_k, t_k = self.step_index, t0
@@ -329,19 +347,19 @@ class OfflineDriver:
                     # stay resident; COSZ is formed on the device every step
                     ti = self.forcing.input_time(t0)
                     if ti != self._raw_t:
-                        self._raw = self.raw_upload.put(
-                            fill=lambda h: self.forcing.block(t_k, out=h))
+                        self._raw, self._raw_up = self._put_block(t_k, "COSZ" in info)
                         self._raw_t = ti
-                    raw = self._raw
-                    if not self.forcing.file_cosz(t0):
+                    raw, upload = self._raw, self._raw_up
+                    if "COSZ" not in info:
                         geo = self.geo
                         solar = timeman.solar_terms(timeman.julian(t0), timeman.yearlen(t0.year))
                 else:
                     raw = self.raw_upload.put(fill=lambda h: self.forcing.raw(step_k, t_k, out=h))
+                    upload = self.raw_upload
                 f = self.raw_fbuf[self.step_index % 2]
                 pre = lambda st, rng: self.engine.forcing_from_ldasin(  # noqa: E731
                     raw, f, stream=st, cols=rng, geo=geo, solar=solar)
-                after, upload = (cur, self.raw_upload.stream), self.raw_upload
+                after = (cur, upload.stream)
             elif self.dev_forcing is not None:
                 clim, fbuf = self.dev_forcing
                 f = fbuf[self.step_index % 2]
@@ -350,7 +368,7 @@ class OfflineDriver:
                     clim, jul, yl, self.forcing.seed, k, f, self.forcing.first_col, stream=st,
                     cols=rng)
                 after, upload = cur, None
-            elif fl is not None:  # LDASIN files, the 12-field form: built into the pinned buffer
+            elif info is not None:  # LDASIN files, the 12-field form: built into the pinned buffer
                 step_k, t_k = self.step_index, t0
                 f = self.upload.put(fill=lambda h: self.forcing(step_k, t_k, out=h))
             else:
@@ -395,6 +413,21 @@ class OfflineDriver:
         self.flush_output()
         return self
 
+    def _put_block(self, t: datetime.datetime, file_cosz: bool):
+        """Upload the LDASIN block of t's input file once; returns the device
+        block and the ForcingUpload whose stream and slot guard it.  With
+        `ingest` (and no COSZ in the file) the file's bytes go up as stored and
+        the engine forms the block's rows (nmp_ldasin_ingest on the upload's
+        stream); otherwise the host builds the block (ncio block)."""
+        if self.ingest is None or file_cosz:
+            return self.raw_upload.put(fill=lambda h: self.forcing.block(t, out=h)), \
+                self.raw_upload
+        up = self.ingest
+        g = up.put(fill=lambda h: self.forcing.grid_raw(t, out=h))
+        blk = self.ingest_blk[up._last]
+        self.engine.ldasin_ingest(g, self.point, blk, stream=up.stream)
+        return blk, up
+
     # ---- output -----------------------------------------------------------------
     def _write_output(self, d: torch.Tensor, path: str, t1: datetime.datetime):
         """One output step's (16, n) fluxes, written on a background thread:
@@ -402,10 +435,8 @@ class OfflineDriver:
         (after the step that produced it), and the writer thread waits for the
         copy, restores the grid order and writes the file while the loop goes
         on stepping.  A buffer is reused once its previous file is written."""
-        if getattr(self, "_writer", None) is None:
-            from concurrent.futures import ThreadPoolExecutor
-            self._writer = ThreadPoolExecutor(1)
-            self._out_host, self._out_fut, self._n_out_w = [None, None], [None, None], 0
+        if self._writer is None:
+            self._writer_init(tuple(d.shape))
         k = self._n_out_w % 2
         self._n_out_w += 1
         if self._out_fut[k] is not None:
@@ -421,11 +452,18 @@ class OfflineDriver:
             ev.synchronize()
             a = h.numpy()
             if self.grid is not None:
-                ncio.write_ldasout(path, self.grid, self.to_grid_order(a), t1)
+                ncio.write_ldasout(path, self.grid, a, t1, cols=getattr(self, "perm", None),
+                                   pool=getattr(self.forcing, "_pool", None))
             else:
                 np.savez(path, time=np.array(t1.isoformat()),
                          fields=np.array(",".join(L.DIAG_OUT)), diag=a)
         self._out_fut[k] = self._writer.submit(job)
+
+    def _writer_init(self, shape):
+        from concurrent.futures import ThreadPoolExecutor
+        self._writer = ThreadPoolExecutor(1)
+        self._out_host = [torch.empty(shape, dtype=self.dtype, pin_memory=True) for _ in range(2)]
+        self._out_fut, self._n_out_w = [None, None], 0
 
     def flush_output(self):
         """Wait until every output file issued so far is written (raises a

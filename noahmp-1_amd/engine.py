@@ -250,6 +250,24 @@ class Engine:
             self._h, hi - lo, n, _ptr(ldasin, lo), _ptr(geo, lo), sd, cd, ha0, _ptr(out, lo),
             C.c_void_p(s.cuda_stream)), "nmp_forcing_from_ldasin_geo")
 
+    def ldasin_ingest(self, grid_be: torch.Tensor, point: torch.Tensor, out: torch.Tensor,
+                      stream=None):
+        """nmp_ldasin_ingest: rows T2D..LWDOWN of the (NLDASIN, n) fp32 block
+        `out` from an LDASIN file's bytes: grid_be = (8, npts) 4-byte words,
+        the file's big-endian fp32 grids in layout.LDASIN order; column c takes
+        grid point point[c] (int32, (n,)).  The COSZ row is left as it is."""
+        n = int(out.shape[1])
+        assert grid_be.dim() == 2 and grid_be.shape[0] == L.NLDASIN - 1
+        assert grid_be.element_size() == 4 and grid_be.is_contiguous()
+        assert point.shape == (n,) and point.dtype == torch.int32 and point.is_contiguous()
+        assert out.shape == (L.NLDASIN, n) and out.dtype == torch.float32 and out.is_contiguous()
+        for t in (grid_be, point, out):
+            assert t.device.type == "cuda" and t.device.index == self.device
+        s = stream if stream is not None else torch.cuda.current_stream(self.device)
+        _lib.check(self._lib.nmp_ldasin_ingest(self._h, n, n, int(grid_be.shape[1]),
+                                               _ptr(grid_be, 0), _ptr(point, 0), _ptr(out, 0),
+                                               C.c_void_p(s.cuda_stream)), "nmp_ldasin_ingest")
+
     # ---- the reference's other public routines (nmp_frh2o / nmp_calhum) ------
     def frh2o(self, sltyp, tkelv, smc, sh2o, status=None, stream=None):
         """frh2o (func.f90:4494-4598) elementwise.  Device tensors (engine

@@ -300,17 +300,50 @@ class LdasinForcing:
         # the latitude factors of COSZ, once (timeman.cosz evaluates the same
         # numpy functions on the same values every step)
         self._sincos_lat = (np.sin(self.lat), np.cos(self.lat))
+        # file grid point of each engine column: one gather per variable
+        self._gidx = np.asarray(grid.index)[self.cols]
         self.threads = max(1, int(threads if threads is not None else
                                   os.environ.get("NMP_HOST_THREADS", 8)))
-        self._pool = None
+        # shared by the read-ahead thread (_load) and the caller (_chunks);
+        # its threads start on first use
+        from concurrent.futures import ThreadPoolExecutor
+        self._pool = ThreadPoolExecutor(self.threads) if self.threads > 1 else None
 
     def input_time(self, t: datetime.datetime) -> datetime.datetime:
         k = (t - self.begin) // self.every
         return self.begin + k * self.every
 
     def _load(self, ti: datetime.datetime) -> dict:
-        raw = read_ldasin(ldasin_path(self.indir, ti))
-        return {k: self.grid.columns(v)[self.cols] for k, v in raw.items()}
+        """This rank's columns of every variable of the input time's file, in
+        engine order and native byte order: one gather per variable straight
+        from the mapped file through the composite index (engine column ->
+        grid point), the variables on the provider's threads.  The values are
+        read_ldasin's, selected by grid.columns and then `cols`."""
+        path = ldasin_path(self.indir, ti)
+        if not os.path.isfile(path):
+            raise FileNotFoundError(path)
+        f = netcdf_file(path, "r", mmap=True)
+        out = {}
+        try:
+            names = list(f.variables)
+
+            def one(k):
+                v = f.variables[k]
+                s = np.asarray(v[0] if v.dimensions[0] == "Time" else v[:]).reshape(-1)
+                out[k] = s[self._gidx].astype(s.dtype.newbyteorder("="))
+            self._map(one, names)
+        finally:
+            f.close()
+        return out
+
+    def _map(self, fn, items):
+        """fn(item) for every item, on the provider's threads."""
+        if self._pool is None or len(items) < 2:
+            for x in items:
+                fn(x)
+            return
+        for fut in [self._pool.submit(fn, x) for x in items]:
+            fut.result()
 
     def fields(self, t: datetime.datetime) -> dict:
         """The LDASIN variables of the step starting at t (this rank's columns).
@@ -337,14 +370,7 @@ class LdasinForcing:
         n = self.lat.shape[0]
         k = min(self.threads, max(1, n // 65536))
         sl = [slice(n * i // k, n * (i + 1) // k) for i in range(k)]
-        if k == 1:
-            fill(sl[0])
-            return
-        if self._pool is None:
-            from concurrent.futures import ThreadPoolExecutor
-            self._pool = ThreadPoolExecutor(self.threads)
-        for fut in [self._pool.submit(fill, c) for c in sl]:
-            fut.result()
+        self._map(fill, sl)
 
     def _cosz(self, fl: dict, t: datetime.datetime, c: slice) -> np.ndarray:
         if "COSZ" in fl:
@@ -405,9 +431,55 @@ class LdasinForcing:
         self._chunks(fill)
         return r
 
+    def variables(self, t: datetime.datetime) -> frozenset:
+        """The variable names of the input file of t (its header only, cached
+        per input time)."""
+        ti = self.input_time(t)
+        if getattr(self, "_vars_t", None) != ti:
+            path = ldasin_path(self.indir, ti)
+            if not os.path.isfile(path):
+                raise FileNotFoundError(path)
+            f = netcdf_file(path, "r", mmap=True)
+            try:
+                self._vars = frozenset(f.variables)
+            finally:
+                f.close()
+            self._vars_t = ti
+        return self._vars
+
+    def point(self) -> np.ndarray:
+        """int32 (n,): the file grid point (row-major index) of each engine
+        column -- nmp_ldasin_ingest's `point`."""
+        return self._gidx.astype(np.int32)
+
+    def grid_raw(self, t: datetime.datetime, out: np.ndarray | None = None):
+        """The input file's 8 LDASIN variables (layout.LDASIN order, COSZ
+        excluded) as the file stores them: (8, npts) big-endian fp32 grids,
+        copied byte for byte into `out` (any 4-byte dtype, e.g. a pinned
+        upload buffer's int32 view), one variable per provider thread.  The
+        engine selects this rank's columns, applies its order and the byte
+        order on the device (nmp_ldasin_ingest)."""
+        path = ldasin_path(self.indir, self.input_time(t))
+        if not os.path.isfile(path):
+            raise FileNotFoundError(path)
+        npts = self.grid.shape[0] * self.grid.shape[1]
+        r = np.empty((L.NLDASIN - 1, npts), ">f4") if out is None else out
+        assert r.shape == (L.NLDASIN - 1, npts) and r.dtype.itemsize == 4
+        f = netcdf_file(path, "r", mmap=True)
+        try:
+            def one(i):
+                v = f.variables[L.LDASIN[i]]
+                s = np.asarray(v[0] if v.dimensions[0] == "Time" else v[:]).reshape(-1)
+                assert s.dtype == np.dtype(">f4"), f"{L.LDASIN[i]}: {s.dtype}"
+                r[i].view(">f4")[...] = s
+            self._map(one, list(range(L.NLDASIN - 1)))
+        finally:
+            f.close()
+        return r
+
     def file_cosz(self, t: datetime.datetime) -> bool:
         """The input file of t carries COSZ (then it, not the solar geometry, is the step's)."""
-        return "COSZ" in self.fields(t)
+        return "COSZ" in self.variables(t)
 
     def geo(self) -> np.ndarray:
         """(3, n) float64 per column: sin lat, cos lat, lon (radians) -- the
@@ -417,9 +489,26 @@ class LdasinForcing:
 
 
 # ---- LDASOUT ----------------------------------------------------------------------
-def write_ldasout(path: str, grid: Grid, diag: np.ndarray, t: datetime.datetime):
-    """The 16 output fluxes (NMP_O_*, (16, n)) on the grid."""
+def write_ldasout(path: str, grid: Grid, diag: np.ndarray, t: datetime.datetime,
+                  cols: np.ndarray | None = None, pool=None):
+    """The 16 output fluxes (NMP_O_*, (16, n)) on the grid.  cols: column j of
+    diag is land point cols[j] (an engine order; default: land-point order).
+    pool: an executor that scatters the fields in parallel."""
     ny, nx = grid.shape
+    kind = "f8" if diag.dtype == np.float64 else "f4"
+    idx = np.asarray(grid.index) if cols is None else np.asarray(grid.index)[cols]
+    # the fields scattered straight into the file's (big-endian) element type
+    full = np.empty((len(L.DIAG_OUT), ny * nx), np.dtype(kind).newbyteorder(">"))
+
+    def one(i):
+        full[i].fill(FILL)
+        full[i][idx] = diag[i]
+    if pool is None:
+        for i in range(len(L.DIAG_OUT)):
+            one(i)
+    else:
+        for fut in [pool.submit(one, i) for i in range(len(L.DIAG_OUT))]:
+            fut.result()
     f = netcdf_file(path, "w")
     try:
         f.createDimension("Time", None)
@@ -427,11 +516,10 @@ def write_ldasout(path: str, grid: Grid, diag: np.ndarray, t: datetime.datetime)
         f.createDimension("west_east", nx)
         f.valid_time = t.isoformat()
         dims = ("Time", "south_north", "west_east")
-        kind = "f8" if diag.dtype == np.float64 else "f4"
         for i, name in enumerate(L.DIAG_OUT):
             v = f.createVariable(name, kind, dims)
             v._FillValue = np.asarray(FILL, kind)
-            v[0] = grid.scatter(diag[i].astype(kind), np.asarray(FILL, kind))
+            v[0] = full[i].reshape(ny, nx)
     finally:
         f.close()
 

@@ -113,8 +113,10 @@ def test_driver_ldasin_block_equals_host_fields(engine_lib, tmp_path, precision)
     host's COSZ every step and the engine forms the 12 fields on each range's
     stream (nmp_forcing_from_ldasin, cosz="host"), or uploads each file's
     variables once per input interval and forms COSZ on the device as well
-    (nmp_forcing_from_ldasin_geo, cosz="device": 24 uploads for 96 steps), or
-    builds the 12 fields on the host (ldasin_upload=False).  All three runs
+    (nmp_forcing_from_ldasin_geo, cosz="device": 24 uploads for 96 steps) --
+    the block built on the host, or the file's bytes uploaded as stored and
+    the block formed on the device (nmp_ldasin_ingest, ingest=True) -- or
+    builds the 12 fields on the host (ldasin_upload=False).  All four runs
     give the same state, ISNOW and LDASOUT files bit for bit, in fp32 and
     fp64, from two host threads or one.  (The device COSZ equals the host's
     on every one of these 3,072 column-steps -- checked first, so a rounding
@@ -139,16 +141,19 @@ def test_driver_ldasin_block_equals_host_fields(engine_lib, tmp_path, precision)
         ncio.write_ldasin(ncio.ldasin_path(str(indir), t), grid, g["forcing"][k], t, extras=False)
         t = t + cfg.input_interval
     runs = []
-    for ldasin, threads, cz in ((False, 1, "host"), (True, 2, "host"), (True, 2, "device")):
-        cfg.outdir = str(tmp_path / f"out_{int(ldasin)}_{cz}")
+    for ldasin, threads, cz, ing in ((False, 1, "host", False), (True, 2, "host", False),
+                                     (True, 2, "device", False), (True, 2, "device", True)):
+        cfg.outdir = str(tmp_path / f"out_{int(ldasin)}_{cz}_{int(ing)}")
         drv = driver.OfflineDriver.from_files(cfg, precision=precision, ldasin_upload=ldasin,
-                                              host_threads=threads, cosz=cz)
-        if cz == "device":
+                                              host_threads=threads, cosz=cz, ingest=ing)
+        if cz == "device" and not ing:
             _check_device_cosz_equals_host(drv, cfg, 96)
         drv.run()
         assert drv.step_index == 96
         uploads = 0 if not ldasin else (96 if cz == "host" else 24)
-        assert (drv.raw_upload.count if drv.raw_upload is not None else 0) == uploads
+        assert (drv.raw_upload.count if drv.raw_upload is not None else 0) == \
+            (0 if ing else uploads)
+        assert (drv.ingest.count if drv.ingest is not None else 0) == (uploads if ing else 0)
         assert drv.upload.count == (0 if ldasin else 96)
         outs = [ncio.read_ldasout(f, grid) for f in sorted(
             glob.glob(os.path.join(cfg.outdir, "*.LDASOUT_DOMAIN1")))]

@@ -168,3 +168,48 @@ def test_forcing_from_ldasin_geo_device_cosz(engine_lib, precision):
     print(f"device COSZ: {mism} of {total} column-steps differ from numpy's by 1 fp32 ulp")
     assert mism <= 1e-5 * total
     eng.close()
+
+
+@pytest.mark.gpu
+def test_ldasin_ingest_equals_host_block(engine_lib, tmp_path):
+    """nmp_ldasin_ingest: an LDASIN file's bytes as stored (ncio grid_raw:
+    big-endian grids, ocean points included) selected, ordered and
+    byte-swapped on the device give the host block's 8 rows (ncio block: the
+    land points in the engine's column order) bit for bit; the COSZ row is not
+    written; a point outside the grid gives NaN rows (no out-of-bounds load)."""
+    import datetime
+    from noahmp_amd import ncio
+    from noahmp_amd.engine import Engine
+    from noahmp_amd.params import Params
+    ny, nx = 40, 64
+    rng = np.random.default_rng(3)
+    mask = rng.uniform(size=(ny, nx)) < 0.6
+    lat = np.broadcast_to(np.linspace(20.0, 50.0, ny)[:, None], (ny, nx))
+    lon = np.broadcast_to(np.linspace(-120.0, -70.0, nx)[None, :], (ny, nx))
+    grid = ncio.Grid(lat, lon, mask)
+    n = grid.n
+    cols = cases.make_columns(n, "conus", Params.builtin().as_dict(), seed=2, julian=100.0)
+    t0 = datetime.datetime(2000, 4, 10)
+    d = tmp_path / "ldasin"
+    d.mkdir()
+    ncio.write_ldasin(ncio.ldasin_path(str(d), t0), grid,
+                      cases.forcing_step(cols, 100.0, 366, 0, seed=2), t0, extras=False)
+    perm = rng.permutation(n)
+    fr = ncio.LdasinForcing(str(d), grid, t0, datetime.timedelta(hours=1), cols=perm, threads=3)
+    want = fr.block(t0, out=np.zeros((L.NLDASIN, n), np.float32))
+    g = fr.grid_raw(t0, out=np.empty((L.NLDASIN - 1, ny * nx), np.int32))
+    point = fr.point()
+    point[5] = ny * nx          # one column outside the grid
+    eng = Engine(Params.builtin(), L.CASE_NML_OPTIONS, device=0, precision=4)
+    out = torch.full((L.NLDASIN, n), -3.0, dtype=torch.float32, device=DEV)
+    eng.ldasin_ingest(torch.as_tensor(g, device=DEV), torch.as_tensor(point, device=DEV), out)
+    torch.cuda.synchronize()
+    got = out.cpu().numpy()
+    ci = L.LDASIN.index("COSZ")
+    ok = np.ones(n, bool)
+    ok[5] = False
+    assert np.array_equal(np.delete(got, ci, 0)[:, ok].view(np.int32),
+                          np.delete(want, ci, 0)[:, ok].view(np.int32))
+    assert np.isnan(np.delete(got, ci, 0)[:, 5]).all()
+    assert (got[ci] == -3.0).all()
+    eng.close()

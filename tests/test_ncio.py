@@ -125,6 +125,18 @@ def test_ldasout_round_trip(tmp_path, ref_params):
     assert np.array_equal(bits(ncio.read_ldasout(p, grid)), bits(diag))
     raw = ncio.read_ldasin(p)
     assert (raw["FSA"][~grid.mask] == ncio.FILL).all()
+    # engine-ordered fluxes (column j = land point perm[j]), scattered on a
+    # pool, fp32 and fp64: the same file contents as the grid-ordered write
+    from concurrent.futures import ThreadPoolExecutor
+    perm = np.random.default_rng(1).permutation(32)
+    for dt in (np.float32, np.float64):
+        d = diag.astype(dt)
+        q = str(tmp_path / f"perm_{np.dtype(dt).itemsize}.nc")
+        with ThreadPoolExecutor(3) as pool:
+            ncio.write_ldasout(q, grid, d[:, perm], T0, cols=perm, pool=pool)
+        got = ncio.read_ldasout(q, grid)
+        assert got.dtype == dt and np.array_equal(bits(got), bits(d))
+        assert (ncio.read_ldasin(q)["FSH"][~grid.mask] == ncio.FILL).all()
 
 
 def test_trajectory_fixture_fits_the_files(tmp_path):

@@ -10,7 +10,9 @@ precision: the 12 forcing fields built on the host and uploaded (48 B per
 column per step in fp32, 96 in fp64), the LDASIN block (the files' 8
 variables + COSZ, fp32, 36 B) expanded on the device (nmp_forcing_from_ldasin),
 and that block uploaded once per input file with COSZ formed on the device
-(cosz="device", nmp_forcing_from_ldasin_geo: no upload between files).
+(cosz="device", nmp_forcing_from_ldasin_geo: no upload between files), built
+on the host or -- the default -- formed on the device from the file's bytes
+as stored (ingest, nmp_ldasin_ingest: the host only copies them).
 After 4 warm-up steps the remaining steps are timed, wall clock between two
 synchronizes, with the driver's own per-phase host times (`phase_s`: LDASIN
 file reads, forcing build + upload enqueue, launch enqueue, output gather +
@@ -46,32 +48,34 @@ def write_namelist(d: str) -> str:
     return p
 
 
-def time_driver(cfg, precision, ldasin, warm, steps, threads, cosz="host"):
+def time_driver(cfg, precision, ldasin, warm, steps, threads, cosz="host", ingest=False):
     import torch
     t0 = time.perf_counter()
     drv = driver.OfflineDriver.from_files(cfg, precision=precision, ldasin_upload=ldasin,
-                                          host_threads=threads, cosz=cosz)
+                                          host_threads=threads, cosz=cosz, ingest=ingest)
     setup = time.perf_counter() - t0
     drv.run(nsteps=warm)
     torch.cuda.synchronize()
     drv.phase_s.clear()
     n_written = len(drv.written)
-    up0 = (drv.raw_upload or drv.upload).count
+    upl = drv.ingest or drv.raw_upload or drv.upload
+    up0 = upl.count
     t0 = time.perf_counter()
     drv.run(nsteps=steps)
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
     n = drv.cs.ncol
     outs = len(drv.written) - n_written
-    bpc = 4 * L.NLDASIN if drv.raw_upload is not None else precision * L.NFORCING
-    puts = (drv.raw_upload or drv.upload).count - up0
+    puts = upl.count - up0
+    bytes_per_put = upl.host[0].numel() * upl.host[0].element_size()
     kind = "12 fields" if drv.raw_upload is None else (
+        "file bytes, device ingest + cosz" if drv.ingest is not None else
         "ldasin block + device cosz" if drv.geo is not None else "ldasin block")
     res = {"precision": precision, "upload": kind, "host_threads": threads, "ncol": n,
            "steps": steps, "output_steps": outs, "uploads": puts,
            "wall_s": el, "ms_per_step": el * 1e3 / steps, "colsteps_per_s": n * steps / el,
            "phase_ms_per_step": {k: v * 1e3 / steps for k, v in drv.phase_s.items()},
-           "pcie_up_bytes_per_step": bpc * n * puts / steps,
+           "pcie_up_bytes_per_step": bytes_per_put * puts / steps,
            "pcie_down_bytes_per_output_step": L.NDIAG_OUT * precision * n,
            "setup_s": setup,
            "status_nonzero_cols": int((drv.cs.status != 0).sum().item())}
@@ -129,9 +133,11 @@ def main():
         # round 5's path (12 fields, one host thread), the threaded host build,
         # and the LDASIN block expanded on the device
         # and the block once per file with COSZ formed on the device
-        for ldasin, threads, cz in ((False, 1, "host"), (False, a.threads, "host"),
-                                    (True, a.threads, "host"), (True, a.threads, "device")):
-            r, st, drv = time_driver(cfg, prec, ldasin, a.warm, a.steps, threads, cz)
+        for ldasin, threads, cz, ing in ((False, 1, "host", False), (False, a.threads, "host", False),
+                                         (True, a.threads, "host", False),
+                                         (True, a.threads, "device", False),
+                                         (True, a.threads, "device", True)):
+            r, st, drv = time_driver(cfg, prec, ldasin, a.warm, a.steps, threads, cz, ing)
             states.append(st)
             r["state_equals_first_run"] = bool(np.array_equal(states[0].view(np.uint8),
                                                               st.view(np.uint8)))
