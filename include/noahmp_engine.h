@@ -22,7 +22,8 @@
  *   nmp_sflx_column                                         core/module_noahmp_func.f90:66-476
  * nmp_forcing_from_ldasin,    the forcing arguments of noahmp_sflx (:72-74) from the LDASIN
  *   nmp_forcing_from_ldasin_geo, variables the namelist's input files carry (run/case.nml:6-7)
- *   nmp_ldasin_ingest
+ *   nmp_ldasin_ingest,
+ *   nmp_ldasout_grid         (and the LDASOUT file's grids from the step's diagnostics)
  * nmp_frh2o, nmp_frh2o_host   frh2o (public routine)        core/module_noahmp_func.f90:4494-4598
  * nmp_calhum, nmp_calhum_host calhum (public by default)     core/module_noahmp_func.f90:3958-3984
  * nmp_state_from_aos          layout bridge from noahmp_state_t records
@@ -354,6 +355,18 @@ int nmp_forcing_from_ldasin_geo(nmp_engine* eng, int64_t ncol, int64_t ld, const
  * here.  Device pointers, enqueued on `stream`. */
 int nmp_ldasin_ingest(nmp_engine* eng, int64_t ncol, int64_t ld, int64_t npts,
                       const void* grid_be, const int32_t* point, float* ldasin, void* stream);
+
+/* The output side's mirror: nfield diagnostics of ncol columns (engine
+ * precision, field-major, leading dimension ld -- e.g. the NMP_O_* fluxes of
+ * nmp_step's diag at level 1) onto the LDASOUT file's grids as a netCDF-3
+ * file stores them: grid_be = nfield grids of npts points of big-endian
+ * engine-precision reals, `fill` (rounded to the engine precision) where no
+ * column lands; column c goes to grid point point[c] (a point outside
+ * [0, npts) is skipped).  A host then writes the bytes as they are.  Device
+ * pointers, enqueued on `stream`. */
+int nmp_ldasout_grid(nmp_engine* eng, int64_t ncol, int64_t ld, int64_t npts, int nfield,
+                     const void* diag, const int32_t* point, double fill, void* grid_be,
+                     void* stream);
 
 int nmp_run(nmp_engine* eng, int64_t ncol, int64_t ld, const float zsoil[4], float dt,
             float julian0, int32_t yearlen, int32_t nsteps, void* state, int32_t* isnow,

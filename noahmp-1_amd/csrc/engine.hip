@@ -407,6 +407,21 @@ int nmp_ldasin_ingest(nmp_engine* eng, int64_t ncol, int64_t ld, int64_t npts,
              : NMP_E_DEVICE;
 }
 
+int nmp_ldasout_grid(nmp_engine* eng, int64_t ncol, int64_t ld, int64_t npts, int nfield,
+                     const void* diag, const int32_t* point, double fill, void* grid_be,
+                     void* stream) {
+  if (!eng || ncol < 0 || ld < ncol || ld >= kMaxColumns || npts < 0 || npts >= kMaxColumns ||
+      nfield < 0 || nfield > NMP_NDIAG_FULL)
+    return NMP_E_ARG;
+  if (npts == 0 || nfield == 0) return NMP_OK;
+  if (!grid_be || (ncol > 0 && (!diag || !point))) return NMP_E_ARG;
+  if (ensure_device(eng->device) != NMP_OK) return NMP_E_DEVICE;
+  return nmp::launch_ldasout_grid(eng->precision, ncol, ld, npts, nfield, diag, point, fill,
+                                  grid_be, static_cast<hipStream_t>(stream)) == hipSuccess
+             ? NMP_OK
+             : NMP_E_DEVICE;
+}
+
 int nmp_forcing_from_ldasin_geo(nmp_engine* eng, int64_t ncol, int64_t ld, const float* ldasin,
                                 const double* geo, double sin_decl, double cos_decl, double ha0,
                                 void* forcing, void* stream) {

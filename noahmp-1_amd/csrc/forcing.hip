@@ -17,6 +17,7 @@
 // forcing fields of one step.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdint>
 
 #include "noahmp_engine.h"
@@ -215,6 +216,71 @@ hipError_t launch_ldasin_ingest(int64_t ncol, int64_t ld, int64_t npts, const vo
   hipLaunchKernelGGL(ldasin_ingest_kernel, dim3((unsigned)grid), dim3(256), 0, stream, ncol, ld,
                      npts, static_cast<const uint32_t*>(grid_be), point, block);
   return hipGetLastError();
+}
+
+// The output side's mirror (nmp_ldasout_grid): nfield diagnostics of ncol
+// columns (engine precision T, field-major, leading dimension ld) onto the
+// file's grids as a netCDF-3 file stores them -- big-endian T, npts points
+// per field, `fill` where no column lands -- so the host writes the bytes
+// as they are.  One pass fills the grids, a second scatters the columns.
+template <class T, class W>
+__global__ __launch_bounds__(256) void grid_fill_kernel(int64_t total, W fill_be,
+                                                        W* __restrict__ grid_be) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x)
+    grid_be[i] = fill_be;
+}
+
+template <class T, class W>
+__global__ __launch_bounds__(256) void grid_scatter_kernel(int64_t ncol, int64_t ld, int64_t npts,
+                                                           int nfield, const W* __restrict__ diag,
+                                                           const int32_t* __restrict__ point,
+                                                           W* __restrict__ grid_be) {
+  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= ncol) return;
+  const int64_t p = point[c];
+  if (p < 0 || p >= npts) return;  // outside the grid: never an out-of-bounds store
+  for (int f = 0; f < nfield; ++f) {
+    const W w = diag[f * ld + c];
+    if constexpr (sizeof(W) == 4)
+      grid_be[f * npts + p] = __builtin_bswap32(w);
+    else
+      grid_be[f * npts + p] = __builtin_bswap64(w);
+  }
+}
+
+template <class T, class W>
+static hipError_t launch_grid_t(int64_t ncol, int64_t ld, int64_t npts, int nfield,
+                                const void* diag, const int32_t* point, double fill,
+                                void* grid_be, hipStream_t stream) {
+  const T f = (T)fill;
+  W fw;
+  __builtin_memcpy(&fw, &f, sizeof(W));
+  if constexpr (sizeof(W) == 4)
+    fw = __builtin_bswap32(fw);
+  else
+    fw = __builtin_bswap64(fw);
+  const int64_t total = (int64_t)nfield * npts;
+  const int64_t fgrid = std::min<int64_t>((total + 255) / 256, 8192);
+  hipLaunchKernelGGL((grid_fill_kernel<T, W>), dim3((unsigned)fgrid), dim3(256), 0, stream, total,
+                     fw, static_cast<W*>(grid_be));
+  const int64_t grid = (ncol + 255) / 256;
+  if (grid > 0)
+    hipLaunchKernelGGL((grid_scatter_kernel<T, W>), dim3((unsigned)grid), dim3(256), 0, stream,
+                       ncol, ld, npts, nfield, static_cast<const W*>(diag), point,
+                       static_cast<W*>(grid_be));
+  return hipGetLastError();
+}
+
+hipError_t launch_ldasout_grid(int precision, int64_t ncol, int64_t ld, int64_t npts, int nfield,
+                               const void* diag, const int32_t* point, double fill, void* grid_be,
+                               hipStream_t stream) {
+  if (npts == 0 || nfield == 0) return hipSuccess;
+  if (precision == 4)
+    return launch_grid_t<float, uint32_t>(ncol, ld, npts, nfield, diag, point, fill, grid_be,
+                                          stream);
+  return launch_grid_t<double, uint64_t>(ncol, ld, npts, nfield, diag, point, fill, grid_be,
+                                         stream);
 }
 
 }  // namespace nmp

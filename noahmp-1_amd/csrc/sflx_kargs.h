@@ -69,6 +69,10 @@ hipError_t launch_forcing_ldasin(int precision, int64_t ncol, int64_t ld, const 
 // csrc/forcing.hip: an LDASIN file's big-endian grids -> the block's 8 rows
 hipError_t launch_ldasin_ingest(int64_t ncol, int64_t ld, int64_t npts, const void* grid_be,
                                 const int32_t* point, float* block, hipStream_t stream);
+// csrc/forcing.hip: diagnostics -> the LDASOUT file's big-endian grids
+hipError_t launch_ldasout_grid(int precision, int64_t ncol, int64_t ld, int64_t npts, int nfield,
+                               const void* diag, const int32_t* point, double fill, void* grid_be,
+                               hipStream_t stream);
 
 // csrc/routines.hip: the reference's public routines frh2o / calhum over n
 // elements (device pointers, engine precision; math 0 = the fp32 "ref" policy)

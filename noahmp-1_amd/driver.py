@@ -239,8 +239,14 @@ class OfflineDriver:
         if write and cfg.output_interval is not None and (
                 not dist.is_initialized() or dist.get_rank() == 0):
             # the output staging buffers up front: a page-locked allocation of
-            # the whole set's fluxes costs tens of ms inside the time loop
-            self._writer_init((L.NDIAG_OUT, total))
+            # the whole set's fluxes costs tens of ms inside the time loop (the
+            # file's grids in its byte order when the run has a grid)
+            if grid is not None:
+                self._writer_init((L.NDIAG_OUT, grid.shape[0] * grid.shape[1]),
+                                  torch.int32 if self.dtype == torch.float32 else torch.int64)
+            else:
+                self._writer_init((L.NDIAG_OUT, total))
+        self._out_point = None
 
     @classmethod
     def from_files(cls, cfg: Config, device: int = 0, params: Params | None = None,
@@ -431,20 +437,36 @@ class OfflineDriver:
     # ---- output -----------------------------------------------------------------
     def _write_output(self, d: torch.Tensor, path: str, t1: datetime.datetime):
         """One output step's (16, n) fluxes, written on a background thread:
-        d is copied into one of two pinned host buffers on the current stream
-        (after the step that produced it), and the writer thread waits for the
-        copy, restores the grid order and writes the file while the loop goes
-        on stepping.  A buffer is reused once its previous file is written."""
+        on the current stream (after the step that produced them) the engine
+        lays them on the file's grids in its byte order (nmp_ldasout_grid)
+        and they are copied into one of two pinned host buffers; the writer
+        thread waits for the copy and writes the header and the bytes
+        (ncio.write_ldasout_grids) while the loop goes on stepping.  A buffer
+        is reused once its previous file is written."""
+        src = d
+        if self.grid is not None:
+            if self._out_point is None:
+                perm = getattr(self, "perm", None)
+                idx = np.asarray(self.grid.index)
+                self._out_point = torch.as_tensor(
+                    (idx if perm is None else idx[perm]).astype(np.int32), device=self.dev)
+                npts = self.grid.shape[0] * self.grid.shape[1]
+                self._out_dev = torch.empty((L.NDIAG_OUT, npts), device=self.dev,
+                                            dtype=torch.int32 if d.dtype == torch.float32
+                                            else torch.int64)
+            self.engine.ldasout_grid(d, self._out_point, self._out_dev, float(ncio.FILL),
+                                     stream=torch.cuda.current_stream(self.dev))
+            src = self._out_dev
         if self._writer is None:
-            self._writer_init(tuple(d.shape))
+            self._writer_init(tuple(src.shape), src.dtype)
         k = self._n_out_w % 2
         self._n_out_w += 1
         if self._out_fut[k] is not None:
             self._out_fut[k].result()
         h = self._out_host[k]
-        if h is None or h.shape != d.shape or h.dtype != d.dtype:
-            h = self._out_host[k] = torch.empty(d.shape, dtype=d.dtype, pin_memory=True)
-        h.copy_(d, non_blocking=True)
+        if h is None or h.shape != src.shape or h.dtype != src.dtype:
+            h = self._out_host[k] = torch.empty(src.shape, dtype=src.dtype, pin_memory=True)
+        h.copy_(src, non_blocking=True)
         ev = torch.cuda.Event()
         ev.record(torch.cuda.current_stream(self.dev))
 
@@ -452,17 +474,18 @@ class OfflineDriver:
             ev.synchronize()
             a = h.numpy()
             if self.grid is not None:
-                ncio.write_ldasout(path, self.grid, a, t1, cols=getattr(self, "perm", None),
-                                   pool=getattr(self.forcing, "_pool", None))
+                ncio.write_ldasout_grids(path, self.grid,
+                                         a.view(">f4" if a.itemsize == 4 else ">f8"), t1)
             else:
                 np.savez(path, time=np.array(t1.isoformat()),
                          fields=np.array(",".join(L.DIAG_OUT)), diag=a)
         self._out_fut[k] = self._writer.submit(job)
 
-    def _writer_init(self, shape):
+    def _writer_init(self, shape, dtype=None):
         from concurrent.futures import ThreadPoolExecutor
         self._writer = ThreadPoolExecutor(1)
-        self._out_host = [torch.empty(shape, dtype=self.dtype, pin_memory=True) for _ in range(2)]
+        dtype = dtype or self.dtype
+        self._out_host = [torch.empty(shape, dtype=dtype, pin_memory=True) for _ in range(2)]
         self._out_fut, self._n_out_w = [None, None], 0
 
     def flush_output(self):

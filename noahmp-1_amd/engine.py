@@ -268,6 +268,24 @@ class Engine:
                                                _ptr(grid_be, 0), _ptr(point, 0), _ptr(out, 0),
                                                C.c_void_p(s.cuda_stream)), "nmp_ldasin_ingest")
 
+    def ldasout_grid(self, diag: torch.Tensor, point: torch.Tensor, out: torch.Tensor,
+                     fill: float, stream=None):
+        """nmp_ldasout_grid: the (nfield, n) diagnostics `diag` (engine
+        precision) onto out = (nfield, npts) words of the engine's size, the
+        file's big-endian grids, `fill` off the columns' points (point: int32
+        (n,))."""
+        nf, n = int(diag.shape[0]), int(diag.shape[1])
+        assert diag.dtype == self.dtype and diag.is_contiguous()
+        assert point.shape == (n,) and point.dtype == torch.int32 and point.is_contiguous()
+        assert out.dim() == 2 and out.shape[0] == nf and out.is_contiguous()
+        assert out.element_size() == self.precision
+        for t in (diag, point, out):
+            assert t.device.type == "cuda" and t.device.index == self.device
+        s = stream if stream is not None else torch.cuda.current_stream(self.device)
+        _lib.check(self._lib.nmp_ldasout_grid(self._h, n, n, int(out.shape[1]), nf, _ptr(diag, 0),
+                                              _ptr(point, 0), float(fill), _ptr(out, 0),
+                                              C.c_void_p(s.cuda_stream)), "nmp_ldasout_grid")
+
     # ---- the reference's other public routines (nmp_frh2o / nmp_calhum) ------
     def frh2o(self, sltyp, tkelv, smc, sh2o, status=None, stream=None):
         """frh2o (func.f90:4494-4598) elementwise.  Device tensors (engine

@@ -102,6 +102,8 @@ def load(build_if_missing: bool = False):
     lib.nmp_forcing_from_ldasin_geo.argtypes = [vp, C.c_int64, C.c_int64, vp, vp, C.c_double,
                                                 C.c_double, C.c_double, vp, vp]
     lib.nmp_ldasin_ingest.argtypes = [vp, C.c_int64, C.c_int64, C.c_int64, vp, vp, vp, vp]
+    lib.nmp_ldasout_grid.argtypes = [vp, C.c_int64, C.c_int64, C.c_int64, C.c_int, vp, vp,
+                                     C.c_double, vp, vp]
     lib.nmp_run.argtypes = [vp, C.c_int64, C.c_int64, f32p, C.c_float, C.c_float, C.c_int32,
                             C.c_int32, vp, vp, vp, vp, vp, C.c_int64, C.c_int32, vp, C.c_int, vp,
                             vp]
@@ -133,7 +135,7 @@ def load(build_if_missing: bool = False):
     return lib
 
 
-EXPORTED_SYMBOLS = ["nmp_read_tables", "nmp_init", "nmp_step", "nmp_step_binned", "nmp_rebin", "nmp_forcing_synth", "nmp_forcing_from_ldasin", "nmp_forcing_from_ldasin_geo", "nmp_ldasin_ingest",
+EXPORTED_SYMBOLS = ["nmp_read_tables", "nmp_init", "nmp_step", "nmp_step_binned", "nmp_rebin", "nmp_forcing_synth", "nmp_forcing_from_ldasin", "nmp_forcing_from_ldasin_geo", "nmp_ldasin_ingest", "nmp_ldasout_grid",
                     "nmp_run", "nmp_run_out", "nmp_frh2o", "nmp_frh2o_host", "nmp_calhum",
                     "nmp_calhum_host",
                     "nmp_state_from_aos", "nmp_sflx_columns", "nmp_sflx_column",

@@ -524,6 +524,54 @@ def write_ldasout(path: str, grid: Grid, diag: np.ndarray, t: datetime.datetime,
         f.close()
 
 
+def _nc_name(s: str) -> bytes:
+    b = s.encode("latin1")
+    return np.array(len(b), ">i4").tobytes() + b + b"\x00" * (-len(b) % 4)
+
+
+def ldasout_header(grid: Grid, kind: str, t: datetime.datetime) -> bytes:
+    """The netCDF-3 classic header write_ldasout's file has (one record of the
+    16 flux variables over (Time, south_north, west_east), the valid_time
+    global attribute, each variable's _FillValue), built from the format's
+    layout: magic, numrecs, dimension / attribute / variable lists, each
+    variable's type, per-record size and data offset."""
+    ny, nx = grid.shape
+    i4 = lambda v: np.array(v, ">i4").tobytes()  # noqa: E731
+    item = np.dtype(kind).itemsize
+    nc_type = {4: 5, 8: 6}[item]                 # NC_FLOAT, NC_DOUBLE
+    fill = np.asarray(FILL, np.dtype(kind).newbyteorder(">")).tobytes()
+    h = [b"CDF\x01", i4(1), i4(10), i4(3)]       # NC_DIMENSION, 3 dims
+    for name, n in (("Time", 0), ("south_north", ny), ("west_east", nx)):
+        h += [_nc_name(name), i4(n)]
+    vt = t.isoformat().encode("latin1")
+    h += [i4(12), i4(1), _nc_name("valid_time"), i4(2), i4(len(vt)), vt,
+          b"\x00" * (-len(vt) % 4)]               # NC_ATTRIBUTE, NC_CHAR
+    h += [i4(11), i4(len(L.DIAG_OUT))]           # NC_VARIABLE
+    vsize = ny * nx * item
+    vsize += -vsize % 4
+    metas = []
+    for name in L.DIAG_OUT:
+        metas.append([_nc_name(name), i4(3), i4(0), i4(1), i4(2), i4(12), i4(1),
+                      _nc_name("_FillValue"), i4(nc_type), i4(1), fill, i4(nc_type), i4(vsize)])
+    size = sum(len(x) for x in h) + sum(sum(len(x) for x in m) + 4 for m in metas)
+    for i, m in enumerate(metas):
+        h += m + [i4(size + i * vsize)]         # begin (32-bit offsets, version 1)
+    return b"".join(h)
+
+
+def write_ldasout_grids(path: str, grid: Grid, grids_be: np.ndarray, t: datetime.datetime):
+    """An LDASOUT file from the 16 fluxes already on the file's grids in its
+    byte order (nmp_ldasout_grid's output: (16, npts) big-endian fp32 or
+    fp64, FILL off the land points): the header and the bytes, one write --
+    the same file write_ldasout produces from the columns."""
+    kind = {4: "f4", 8: "f8"}[grids_be.dtype.itemsize]
+    ny, nx = grid.shape
+    assert grids_be.shape == (len(L.DIAG_OUT), ny * nx) and grids_be.flags.c_contiguous
+    with open(path, "wb") as f:
+        f.write(ldasout_header(grid, kind, t))
+        f.write(memoryview(grids_be).cast("B"))
+
+
 def read_ldasout(path: str, grid: Grid) -> np.ndarray:
     raw = read_ldasin(path)
     return np.stack([grid.columns(raw[name]) for name in L.DIAG_OUT])

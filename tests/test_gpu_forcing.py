@@ -213,3 +213,43 @@ def test_ldasin_ingest_equals_host_block(engine_lib, tmp_path):
     assert np.isnan(np.delete(got, ci, 0)[:, 5]).all()
     assert (got[ci] == -3.0).all()
     eng.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("precision", [4, 8])
+def test_ldasout_grid_equals_host_scatter(engine_lib, precision):
+    """nmp_ldasout_grid: 16 fluxes of n columns (engine precision) laid on
+    the file's grids in its byte order on the device equal the host's
+    grid.scatter with FILL, converted to big-endian, bit for bit; a point
+    outside the grid is skipped."""
+    from noahmp_amd import ncio
+    from noahmp_amd.engine import Engine
+    from noahmp_amd.params import Params
+    dt = np.float32 if precision == 4 else np.float64
+    ny, nx = 37, 53
+    rng = np.random.default_rng(4)
+    mask = rng.uniform(size=(ny, nx)) < 0.7
+    grid = ncio.Grid(np.zeros((ny, nx)), np.zeros((ny, nx)), mask)
+    n = grid.n
+    diag = rng.normal(size=(L.NDIAG_OUT, n)).astype(dt)
+    perm = rng.permutation(n)
+    point = np.asarray(grid.index)[perm].astype(np.int32)
+    want = np.stack([grid.scatter(diag[i], np.asarray(ncio.FILL, dt)).reshape(-1)
+                     for i in range(L.NDIAG_OUT)]).astype(np.dtype(dt).newbyteorder(">"))
+    eng = Engine(Params.builtin(), L.CASE_NML_OPTIONS, device=0, precision=precision)
+    iv = torch.int32 if precision == 4 else torch.int64
+    out = torch.zeros((L.NDIAG_OUT, ny * nx), dtype=iv, device=DEV)
+    d = torch.as_tensor(np.ascontiguousarray(diag[:, perm]), device=DEV)
+    bad = point.copy()
+    bad[7] = -1
+    eng.ldasout_grid(d, torch.as_tensor(point, device=DEV), out, float(ncio.FILL))
+    torch.cuda.synchronize()
+    got = out.cpu().numpy().view(want.dtype)
+    assert np.array_equal(got.view(np.uint8), want.view(np.uint8))
+    eng.ldasout_grid(d, torch.as_tensor(bad, device=DEV), out, float(ncio.FILL))
+    torch.cuda.synchronize()
+    got = out.cpu().numpy().view(want.dtype)
+    skip = point[7]
+    want[:, skip] = np.asarray(ncio.FILL, dt)
+    assert np.array_equal(got.view(np.uint8), want.view(np.uint8))
+    eng.close()

@@ -154,3 +154,23 @@ def test_trajectory_fixture_fits_the_files(tmp_path):
 def load_params_dict():
     from noahmp_amd.params import Params
     return Params.builtin().as_dict()
+
+
+def test_ldasout_from_grids_is_the_same_file(tmp_path, ref_params):
+    """ncio.write_ldasout_grids (the header built from the netCDF-3 layout
+    plus the fluxes already on the file's big-endian grids, as
+    nmp_ldasout_grid forms them on the device) writes the very bytes of
+    write_ldasout (scipy's netcdf writer) -- fp32 and fp64, a grid with ocean
+    points, two valid times."""
+    cols = cases.make_columns(32, "mixed", ref_params, seed=8)
+    grid = grid_for(cols)
+    for dt in (np.float32, np.float64):
+        diag = np.random.default_rng(2).normal(size=(L.NDIAG_OUT, 32)).astype(dt)
+        full = np.stack([grid.scatter(diag[i], np.asarray(ncio.FILL, dt)).reshape(-1)
+                         for i in range(L.NDIAG_OUT)]).astype(np.dtype(dt).newbyteorder(">"))
+        for t in (T0, T0 + datetime.timedelta(hours=3, minutes=30)):
+            a, b = str(tmp_path / "a.nc"), str(tmp_path / "b.nc")
+            ncio.write_ldasout(a, grid, diag, t)
+            ncio.write_ldasout_grids(b, grid, full, t)
+            assert open(a, "rb").read() == open(b, "rb").read()
+            assert np.array_equal(bits(ncio.read_ldasout(b, grid)), bits(diag))
