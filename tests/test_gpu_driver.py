@@ -215,8 +215,10 @@ def test_offline_cli_runs_a_netcdf_case(engine_lib, tmp_path):
     assert d.shape == (L.NDIAG_OUT, 32) and np.isfinite(d).all()
 
 
-def _write_netcdf_case(tmp_path, g):
-    """static / init / LDASIN files of the traj_casenml columns + a namelist (900-s steps)."""
+def _write_netcdf_case(tmp_path, g, extras=True):
+    """static / init / LDASIN files of the traj_casenml columns + a namelist
+    (900-s steps); extras=False: standard HRLDAS files (no COSZ / CO2AIR /
+    O2AIR), which the driver ingests on the device."""
     from noahmp_amd import ncio
     from test_config import write_case
     from test_ncio import grid_for
@@ -233,7 +235,7 @@ def _write_netcdf_case(tmp_path, g):
     ncio.write_static(str(static), cols, grid)
     ncio.write_state(str(init), grid, g["state0"], g["isnow0"], cfg.begdatetime)
     for k, t in enumerate([cfg.begdatetime + i * cfg.timestep for i in range(96)]):
-        ncio.write_ldasin(ncio.ldasin_path(str(indir), t), grid, g["forcing"][k], t)
+        ncio.write_ldasin(ncio.ldasin_path(str(indir), t), grid, g["forcing"][k], t, extras=extras)
     return nml, grid
 
 
@@ -247,7 +249,8 @@ def _driver_rank(rank, world, port, nml, out_dir):
     drv = driver.OfflineDriver.from_files(cfg)
     drv.run()
     np.savez(os.path.join(out_dir, f"rank{rank}.npz"), state=drv.cs.state.cpu().numpy(),
-             isnow=drv.cs.isnow.cpu().numpy(), cols=drv.cols_index)
+             isnow=drv.cs.isnow.cpu().numpy(), cols=drv.cols_index,
+             ingest=drv.ingest is not None and drv.ingest.count > 0)
     dist.barrier()
     drv.engine.close()
     dist.destroy_process_group()
@@ -289,6 +292,43 @@ def test_driver_multi_rank_files_equal_reference(engine_lib, tmp_path, world):
             assert np.array_equal(z["isnow"], g["isnows"][-1][idx])
             seen.append(idx)
     assert np.array_equal(np.sort(np.concatenate(seen)), np.arange(32))
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_driver_multi_rank_ingest_equals_single_rank(engine_lib, tmp_path, world):
+    """Standard HRLDAS files under a process group: every rank uploads each
+    file's bytes and ingests its own shard on the device (nmp_ldasin_ingest,
+    its block of the coherent order), forms COSZ there, and rank 0 gathers
+    and writes LDASOUT from the device-formed grids (nmp_ldasout_grid).  The
+    LDASOUT files are byte-identical to a single-rank run that builds the 12
+    forcing fields on the host, and every rank's final state equals that
+    run's columns bit for bit."""
+    import socket
+    import torch.multiprocessing as mp
+    g = load("traj_casenml.npz")
+    nml, grid = _write_netcdf_case(tmp_path, g, extras=False)
+    cfg = config.Config(str(nml))
+    out_multi = cfg.outdir
+    cfg.outdir = str(tmp_path / "single")
+    one = driver.OfflineDriver.from_files(cfg, ldasin_upload=False).run()
+    assert one.upload.count == 96
+    ref_state = one.to_grid_order(one.cs.state.cpu().numpy())
+    one.engine.close()
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    mp.start_processes(_driver_rank, args=(world, port, str(nml), str(tmp_path)), nprocs=world,
+                       start_method="spawn")
+    multi = sorted(glob.glob(os.path.join(out_multi, "*.LDASOUT_DOMAIN1")))
+    single = sorted(glob.glob(os.path.join(cfg.outdir, "*.LDASOUT_DOMAIN1")))
+    assert len(multi) == len(single) == 8
+    for a, b in zip(multi, single):
+        assert os.path.basename(a) == os.path.basename(b)
+        assert open(a, "rb").read() == open(b, "rb").read(), a
+    for r in range(world):
+        with np.load(tmp_path / f"rank{r}.npz") as z:
+            assert z["ingest"], "the rank took the device-ingest path"
+            assert bit_equal(z["state"], ref_state[:, z["cols"]]).all(), r
 
 
 def test_driver_device_forcing_equals_engine_steps(engine_lib, tmp_path):
