@@ -10,6 +10,9 @@
 !   mode "runl": as "run", with the step's LDASIN block (nmp_ldasin, taken
 !                from the forcing's T2D Q2D U2D V2D PSFC RAINRATE SWDOWN LWDOWN
 !                COSZ) and nmp_ldasin_forcing, the forcing formed on the device;
+!   mode "runc": as "runl", on forcing whose 8 LDASIN variables hold over
+!                groups of 4 steps: steps 2-4 of a group upload only COSZ
+!                (nmp_ldasin_cosz_only);
 !   mode "sflx": one noahmp_sflx call per column per step with the
 !                reference's 131 arguments (FICEOLD from the step-start ice
 !                fraction, as the reference harness passes it).
@@ -26,7 +29,8 @@
 ! usage: engine_drop_in <run|runl|sflx> <tbl_dir> <in.bin> <out.bin>
 !        engine_drop_in time <tbl_dir> <in.bin> <out.txt> <ncol> <nsteps> <out_every> <pinned>
 !                            [<chunks>]   (noahmp_run's pipeline chunks, default the module's)
-!                            [<ldasin>]   (1: upload the LDASIN block, nmp_ldasin_forcing)
+!                            [<ldasin>]   (1: upload the LDASIN block, nmp_ldasin_forcing;
+!                                          2: and only its COSZ row on 3 steps of 4)
 !   in.bin : int32 n, nsteps, yearlen, options(12); real zsoil(4), dt;
 !            real julian(nsteps); int32 static_i(n,6), isnow(n);
 !            real static_f(n,6), state(n,56), forcing(n,12,nsteps)
@@ -70,8 +74,9 @@ program engine_drop_in
   open(newunit=v, file=trim(fout), access='stream', form='unformatted', status='replace')
   do s = 1, nsteps
      nmp_julian = jul(s)
-     if (trim(mode) == 'run' .or. trim(mode) == 'runl') then
-        nmp_ldasin_forcing = trim(mode) == 'runl'
+     if (trim(mode) == 'run' .or. trim(mode) == 'runl' .or. trim(mode) == 'runc') then
+        nmp_ldasin_forcing = trim(mode) /= 'run'
+        nmp_ldasin_cosz_only = trim(mode) == 'runc' .and. mod(s - 1, 4) /= 0
         if (nmp_ldasin_forcing) then
            nmp_ldasin = frc(:, lmap, s)
         else
@@ -110,6 +115,8 @@ contains
        call get_command_argument(10, arg); read(arg, *) ldasin
     end if
     nmp_ldasin_forcing = ldasin /= 0
+    ! (ldasin 2: the timed steps cycle the nf forcing slices; each slice's
+    ! LDASIN variables are taken to hold for 4 steps, of which 3 upload COSZ only)
     nf = min(nsteps, 4)
     call noahmp_columns(ncol)
     do i = 1, ncol
@@ -133,7 +140,10 @@ contains
     do s = 1, nt + 2
        k = mod(s - 1, nf) + 1
        call system_clock(t0)
-       if (nmp_ldasin_forcing) then         ! the host's own work: filling this step's forcing
+       nmp_ldasin_cosz_only = ldasin == 2 .and. mod(s - 1, 4) /= 0
+       if (nmp_ldasin_cosz_only) then       ! the host's own work: filling this step's forcing
+          nmp_ldasin(:, 9) = lrep(:, 9, k)
+       else if (nmp_ldasin_forcing) then
           nmp_ldasin = lrep(:, :, k)
        else
           nmp_forcing = frep(:, :, k)
@@ -145,7 +155,8 @@ contains
        call system_clock(t2)
        if (s > 2) then
           tfill = tfill + (t1 - t0); trun = trun + (t2 - t1)
-          up = up + merge(4d0 * 9, storage_size(nmp_forcing) / 8d0 * 12, nmp_ldasin_forcing) * ncol
+          up = up + merge(4d0 * merge(1, 9, nmp_ldasin_cosz_only), &
+                          storage_size(nmp_forcing) / 8d0 * 12, nmp_ldasin_forcing) * ncol
           down = down + ncol * (4d0 + storage_size(nmp_diag) / 8d0 * merge(16, 0, nmp_diag_level == 1))
        end if
     end do

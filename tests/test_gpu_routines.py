@@ -414,8 +414,10 @@ def test_fortran_engine_slot_ldasin_block(tmp_path):
     with nmp_forcing_from_ldasin.  Its 96-step trajectory equals, bit for bit,
     mode "run" (12 fields uploaded) on the forcing an HRLDAS host forms from
     the same variables: SFCPRS = PSFC, CO2AIR = 395e-6 PSFC, O2AIR = 0.209 PSFC
-    rounded to fp32 (noahmp-1_amd/ncio.py LdasinForcing, after
-    hrldas_drv_HRLDAS.f90's CO2/O2 volume fractions)."""
+    rounded to fp32 (noahmp-1_amd/ncio.py LdasinForcing).  Mode "runc" on forcing
+    whose 8 LDASIN variables hold over groups of 4 steps uploads only COSZ on
+    3 steps of 4 (`nmp_ldasin_cosz_only`, the other rows resident) and equals
+    the 12-field run on that forcing bit for bit."""
     import subprocess
     from golden_io import load
     from noahmp_amd import layout as L
@@ -432,13 +434,24 @@ def test_fortran_engine_slot_ldasin_block(tmp_path):
     jul = np.array([float(g["julian0"]) + s * dt / 86400.0 for s in range(nsteps)], np.float32)
     frc = np.array(g["forcing"], np.float32)          # (nsteps, 12, n)
     a = {k: L.FORCING.index(k) for k in ("SFCPRS", "PSFC", "CO2AIR", "O2AIR")}
-    psfc = frc[:, a["PSFC"]].astype(np.float64)
-    host = frc.copy()
-    host[:, a["SFCPRS"]] = frc[:, a["PSFC"]]
-    host[:, a["CO2AIR"]] = (395.0e-6 * psfc).astype(np.float32)
-    host[:, a["O2AIR"]] = (0.209 * psfc).astype(np.float32)
+
+    def host_formed(f):
+        psfc = f[:, a["PSFC"]].astype(np.float64)
+        h = f.copy()
+        h[:, a["SFCPRS"]] = f[:, a["PSFC"]]
+        h[:, a["CO2AIR"]] = (395.0e-6 * psfc).astype(np.float32)
+        h[:, a["O2AIR"]] = (0.209 * psfc).astype(np.float32)
+        return h
+    # the 8 LDASIN variables held over groups of 4 steps (hourly files at
+    # 900-s steps), COSZ every step's own: mode "runc" uploads only COSZ on
+    # steps 2-4 of each group (nmp_ldasin_cosz_only)
+    held = frc.copy()
+    for f in ("SFCTMP", "Q2", "UU", "VV", "PSFC", "PRCP", "SOLDN", "LWDN"):
+        i = L.FORCING.index(f)
+        held[:, i] = frc[(np.arange(nsteps) // 4) * 4, i]
     outs = {}
-    for mode, forcing in (("runl", frc), ("run", host)):
+    for mode, forcing in (("runl", frc), ("run", host_formed(frc)), ("runc", held),
+                          ("run_held", host_formed(held))):
         fin, fout = str(tmp_path / f"{mode}.in"), str(tmp_path / f"{mode}.out")
         with open(fin, "wb") as f:
             for a in (np.array([n, nsteps, int(g["yearlen"])], np.int32),
@@ -446,12 +459,14 @@ def test_fortran_engine_slot_ldasin_block(tmp_path):
                       np.array([dt], np.float32), jul, g["static_i"].astype(np.int32),
                       g["isnow0"].astype(np.int32), g["static_f"], g["state0"], forcing):
                 f.write(np.ascontiguousarray(a).tobytes())
-        r = subprocess.run([exe, mode, tbl, fin, fout], capture_output=True, text=True,
-                           timeout=300)
+        r = subprocess.run([exe, mode.split("_")[0], tbl, fin, fout], capture_output=True,
+                           text=True, timeout=300)
         assert r.returncode == 0, r.stdout + r.stderr
         outs[mode] = np.fromfile(fout, np.uint8)
     assert outs["runl"].size == nsteps * 4 * n * (56 + 1 + 58 + 1)
     assert np.array_equal(outs["runl"], outs["run"])
+    assert np.array_equal(outs["runc"], outs["run_held"])
+    assert not np.array_equal(outs["runc"], outs["runl"])  # the held forcing is a different run
 
 
 @pytest.mark.gpu

@@ -36,8 +36,9 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--out", default=None)
     ap.add_argument("--configs", default="1:6:1,1:6:2,1:6:4,1:6:8,1:1:4,0:6:4,1:6:4:1,1:1:4:1,"
-                                          "1:6:8:1",
-                    help="pinned:out_every:chunks[:ldasin],...")
+                                          "1:6:8:1,1:6:4:2,1:6:2:2,1:6:1:2",
+                    help="pinned:out_every:chunks[:ldasin],...; ldasin 2: COSZ only on 3 "
+                         "steps of 4")
     a = ap.parse_args()
     exe = os.path.join(ROOT, "tests", "lib", "engine_drop_in")
     tbl = os.path.join(ROOT, "oracle", "_ref", "tbl")
@@ -71,7 +72,9 @@ def main():
                  "pinned": bool(int(v[3])), "ms_per_noahmp_run": float(v[4]),
                  "ms_host_forcing_fill": float(v[5]), "column_steps_per_s": float(v[6]),
                  "pcie_bytes_up_per_step": float(v[7]), "pcie_bytes_down_per_step": float(v[8]),
-                 "chunks": int(v[9]), "forcing_upload": "ldasin block" if int(v[10]) else "12 fields"}
+                 "chunks": int(v[9]),
+                 "forcing_upload": {0: "12 fields", 1: "ldasin block",
+                                    2: "ldasin block, COSZ only between files"}[int(v[10])]}
             d["pcie_gb_per_s"] = (d["pcie_bytes_up_per_step"] + d["pcie_bytes_down_per_step"]) \
                 / (d["ms_per_noahmp_run"] * 1e-3) / 1e9
             print(json.dumps(d), flush=True)
