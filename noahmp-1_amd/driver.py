@@ -425,7 +425,7 @@ class OfflineDriver:
         `ingest` (and no COSZ in the file) the file's bytes go up as stored and
         the engine forms the block's rows (nmp_ldasin_ingest on the upload's
         stream); otherwise the host builds the block (ncio block)."""
-        if self.ingest is None or file_cosz:
+        if self.ingest is None or file_cosz or not self.forcing.ingestible(t):
             return self.raw_upload.put(fill=lambda h: self.forcing.block(t, out=h)), \
                 self.raw_upload
         up = self.ingest

@@ -442,10 +442,23 @@ class LdasinForcing:
             f = netcdf_file(path, "r", mmap=True)
             try:
                 self._vars = frozenset(f.variables)
+                # the device ingest takes the 8 variables as fp32 grids
+                npts = self.grid.shape[0] * self.grid.shape[1]
+                self._ingestible = all(
+                    k in f.variables and f.variables[k].data.dtype == np.dtype(">f4") and
+                    f.variables[k].data.size in (npts, npts * f.variables[k].data.shape[0])
+                    and f.variables[k].data.shape[-2:] == self.grid.shape
+                    for k in L.LDASIN[:-1])
             finally:
                 f.close()
             self._vars_t = ti
         return self._vars
+
+    def ingestible(self, t: datetime.datetime) -> bool:
+        """The input file of t holds the 8 LDASIN variables as fp32 grids of
+        the run's shape (what grid_raw / nmp_ldasin_ingest take)."""
+        self.variables(t)
+        return self._ingestible
 
     def point(self) -> np.ndarray:
         """int32 (n,): the file grid point (row-major index) of each engine

@@ -54,6 +54,22 @@ def test_header_functions_exported(engine_lib):
         assert getattr(engine_lib, name) is not None
 
 
+def test_probe_library_is_current():
+    """The test-side probe library (__graft_entry__.build(): the shipped
+    sources with narrowed windows, loaded by test_midloop_domain_exit_bit_exact
+    through the same bindings) is built from the current sources: it carries
+    their hash and exports every header function."""
+    import __graft_entry__ as g
+    from noahmp_amd import build as _b
+    if not os.path.exists(g.PROBE_MIDLOOP):
+        pytest.skip("probe library not built (run __graft_entry__.build())")
+    nm = subprocess.run(["nm", "-D", "--defined-only", g.PROBE_MIDLOOP], capture_output=True,
+                        text=True, check=True).stdout
+    missing = set(_lib.EXPORTED_SYMBOLS) - set(re.findall(r"\bT (nmp_\w+)$", nm, re.M))
+    assert not missing, f"stale probe library, rebuild it: missing {sorted(missing)}"
+    assert _b.built_hash(g.PROBE_MIDLOOP) is not None
+
+
 def test_layout_matches_header():
     e = _enum_values(_header())
     for name, (off, _w) in L.STATE_OFF.items():

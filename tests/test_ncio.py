@@ -108,6 +108,36 @@ def test_ldasin_round_trip_and_derived_fields(tmp_path, ref_params):
     sd, cd, ha0 = timeman.solar_terms(timeman.julian(t), 366)
     cz_geo = geo[0] * sd + (geo[1] * cd) * np.cos((ha0 + geo[2]) - np.pi)
     assert np.array_equal(bits(cz_geo.astype(np.float32)), bits(cz))
+    # the device-ingest form: the file's own big-endian fp32 grids, every grid
+    # point, whose land points in prov2's column order are the block's rows
+    assert prov2.ingestible(t) and prov2.variables(t) == frozenset(L.LDASIN[:-1])
+    gr = prov2.grid_raw(t)
+    assert gr.dtype == np.dtype(">f4") and gr.shape == (L.NLDASIN - 1, 40)
+    assert np.array_equal(bits(gr[:, prov2.point()].astype(np.float32)),
+                          bits(np.delete(raw, ci, 0)))
+    # a file holding a variable in fp64 is not ingestible (the driver then
+    # builds the block on the host)
+    from scipy.io import netcdf_file
+    p64 = ncio.ldasin_path(str(d), T0 + datetime.timedelta(hours=1))
+    ncio.write_ldasin(p64, grid, f, T0, extras=False)
+    with netcdf_file(p64, "a") as nc:
+        v = nc.createVariable("T2D_", "f8", ("Time", "south_north", "west_east"))
+        v[0] = np.zeros(grid.shape)
+    prov3 = ncio.LdasinForcing(str(d), grid, T0, datetime.timedelta(hours=1))
+    assert prov3.ingestible(T0 + datetime.timedelta(hours=1))   # extra variables do not matter
+    ncio.write_ldasin(p64, grid, f, T0, extras=False)
+    with netcdf_file(p64, "r") as nc:
+        vs = {k: np.array(nc.variables[k][0]) for k in nc.variables}
+    with netcdf_file(p64, "w") as nc:
+        nc.createDimension("Time", None)
+        nc.createDimension("south_north", 5)
+        nc.createDimension("west_east", 8)
+        for k, a in vs.items():
+            v = nc.createVariable(k, "f8" if k == "T2D" else "f4", ("Time", "south_north",
+                                                                     "west_east"))
+            v[0] = a
+    prov4 = ncio.LdasinForcing(str(d), grid, T0, datetime.timedelta(hours=1))
+    assert not prov4.ingestible(T0 + datetime.timedelta(hours=1))
     # a file with its own CO2AIR / O2AIR has no block form
     ncio.write_ldasin(ncio.ldasin_path(str(d), T0), grid, f, T0, extras=("CO2AIR",))
     assert ncio.LdasinForcing(str(d), grid, T0, datetime.timedelta(hours=1)).raw(0, T0) is None
