@@ -113,6 +113,12 @@ class ForcingUpload:
         self._last = b
         return self.dev[b]
 
+    @property
+    def last_slot(self) -> int:
+        """The buffer slot of the last put (its device buffer and whatever the
+        caller keeps per slot are guarded by the same events)."""
+        return self._last
+
     def consumed_by(self, streams):
         """The last put's device buffer is read by launches on `streams`."""
         evs = []
@@ -430,7 +436,7 @@ class OfflineDriver:
                 self.raw_upload
         up = self.ingest
         g = up.put(fill=lambda h: self.forcing.grid_raw(t, out=h))
-        blk = self.ingest_blk[up._last]
+        blk = self.ingest_blk[up.last_slot]
         self.engine.ldasin_ingest(g, self.point, blk, stream=up.stream)
         return blk, up
 
