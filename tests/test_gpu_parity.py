@@ -1164,3 +1164,66 @@ def test_midloop_domain_exit_bit_exact():
     for run in res["runs"]:
         print(run)
     assert r.returncode == 0 and res["ok"], res
+
+
+def test_full_size_year_sample_vs_reference(engines):
+    """Config #5's grid in fp32 for a whole hourly year on the product path:
+    1,036,800 global columns, opt_veg 2 (carbon on), 8,784 steps of 3,600 s
+    through the bench's two stream ranges, the forcing generated on the device
+    before each range's launch (nmp_forcing_synth), the 16 output fluxes every
+    step.  512 seeded columns are re-run through the reference Fortran itself
+    (oracle/_ref: ref_sflx_run, the time loop in the harness, JULIAN formed
+    there as julian0 + s*dt/86400 in default real) with the forcing the device
+    generated for them: their state and ISNOW after each of 12 chunks of 732
+    steps, and each chunk's last output fluxes, equal the reference's bit for
+    bit.  The year test at 256 columns covers the physics; this one the launch
+    at BASELINE size for as long as config #5 runs."""
+    import ref
+    from noahmp_amd.engine import ColumnState, StreamShards
+    from noahmp_amd.params import Params
+    if not ref.available():
+        pytest.skip("reference oracle not built (oracle/_ref)")
+    P = Params.builtin()
+    opts = dict(L.CASE_NML_OPTIONS, opt_veg=2)
+    otuple = tuple(opts[k] for k in L.OPTION_NAMES)
+    eng = engines(otuple, 4)
+    n, dt, nsteps, nchunk, yl, seed = 1_036_800, 3600.0, 8784, 12, 366, 5
+    cols = cases.make_columns(n, "global", P.as_dict(), seed=seed, julian=0.0)
+    idx = np.sort(np.random.default_rng(seed).choice(n, 512, replace=False))
+    cs = ColumnState.from_host(cols, DEV, torch.float32)
+    clim = torch.as_tensor(cases.climate(cols), device=DEV).float().contiguous()
+    F = torch.empty((2, L.NFORCING, n), device=DEV)
+    diag = torch.zeros((L.NDIAG_OUT, n), device=DEV)
+    per = nsteps // nchunk
+    Fs = torch.empty((per, L.NFORCING, idx.size), device=DEV)
+    idx_dev = torch.as_tensor(idx, device=DEV)
+    ranges = StreamShards(eng, cs, 2)
+    ref.configure(otuple)
+    rec = ref.Records(cols.state[:, idx], cols.isnow[idx], cols.static_f[:, idx],
+                      cols.static_i[:, idx], np.zeros((1, L.NFORCING, idx.size), np.float32))
+    f32 = np.float32
+    cur = torch.cuda.current_stream()
+    for c in range(nchunk):
+        s0 = c * per
+        jul0 = f32(s0 * dt / 86400.0)
+        for s in range(per):
+            jul = jul0 + f32(s) * f32(dt) / f32(86400.0)   # the harness's expression
+            f = F[(s0 + s) % 2]
+            pre = lambda st, rng, f=f, jul=jul, k=s0 + s: eng.forcing_synth(  # noqa: E731
+                clim, float(jul), yl, seed, k, f, stream=st, cols=rng)
+            ranges.step(f, cases.CASE_NML_ZSOIL, dt, float(jul), yl, diag, L.DIAG_OUT_LEVEL,
+                        pre=pre)
+            ranges.join(cur)
+            torch.index_select(f, 1, idx_dev, out=Fs[s])
+        torch.cuda.synchronize()
+        rec.fc = np.ascontiguousarray(Fs.cpu().numpy().transpose(0, 2, 1))
+        ref.run(cases.CASE_NML_ZSOIL, dt, yl, float(jul0), rec, per)
+        got = cs.state.cpu().numpy()[:, idx]
+        gd = diag.cpu().numpy()[:, idx]
+        want_d = rec.dg.T
+        od = np.stack([want_d[L.DIAG_FULL.index(m)] for m in L.DIAG_OUT if m != "T2M"])
+        gd = np.stack([gd[i] for i, m in enumerate(L.DIAG_OUT) if m != "T2M"])
+        assert np.array_equal(cs.isnow.cpu().numpy()[idx], rec.isn), f"chunk {c}: ISNOW differs"
+        ok = bit_equal(got, rec.st.T).all(0) & bit_equal(gd, od).all(0)
+        assert ok.all(), f"chunk {c} (step {s0 + per}): {(~ok).sum()} of {idx.size} columns differ"
+    assert (rec.isn < 0).any() or (cols.isnow[idx] < 0).any()  # snow came and went
