@@ -128,6 +128,12 @@ def test_abi_version_and_errors(engine_lib):
     rec = np.zeros(1, L.sflx_args_dtype())
     assert engine_lib.nmp_sflx_columns(None, rec.ctypes.data, 1) == -1
     assert engine_lib.nmp_sflx_column(None, rec.ctypes.data) == -1
+    # the LDASIN / LDASOUT entries reject a missing engine before any device work
+    assert engine_lib.nmp_forcing_from_ldasin(None, 1, 1, None, None, None) == -1
+    assert engine_lib.nmp_forcing_from_ldasin_geo(None, 1, 1, None, None, 0.0, 1.0, 0.0, None,
+                                                  None) == -1
+    assert engine_lib.nmp_ldasin_ingest(None, 1, 1, 1, None, None, None, None) == -1
+    assert engine_lib.nmp_ldasout_grid(None, 1, 1, 1, 16, None, None, -9999.0, None, None) == -1
 
 
 def test_sflx_args_layout(tmp_path):

@@ -253,3 +253,39 @@ def test_ldasout_grid_equals_host_scatter(engine_lib, precision):
     want[:, skip] = np.asarray(ncio.FILL, dt)
     assert np.array_equal(got.view(np.uint8), want.view(np.uint8))
     eng.close()
+
+
+@pytest.mark.gpu
+def test_ldasin_ldasout_entries_reject_bad_arguments(engine_lib):
+    """The file-format entries check their sizes before launching: a leading
+    dimension below ncol, an empty or oversized grid, too many fields, or a
+    missing pointer return NMP_E_ARG and leave the output untouched; zero
+    columns is a no-op."""
+    import ctypes as C
+    from noahmp_amd.engine import Engine, _ptr
+    from noahmp_amd.params import Params
+    eng = Engine(Params.builtin(), L.CASE_NML_OPTIONS, device=0, precision=4)
+    lib, h = eng._lib, eng._h
+    n, npts = 64, 100
+    g = torch.zeros((L.NLDASIN - 1, npts), dtype=torch.int32, device=DEV)
+    pt = torch.arange(n, dtype=torch.int32, device=DEV)
+    blk = torch.full((L.NLDASIN, n), 7.0, device=DEV)
+    diag = torch.zeros((L.NDIAG_OUT, n), device=DEV)
+    out = torch.full((L.NDIAG_OUT, npts), 5, dtype=torch.int32, device=DEV)
+    s = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+    E_ARG = -1
+    assert lib.nmp_ldasin_ingest(h, n, n - 1, npts, _ptr(g), _ptr(pt), _ptr(blk), s) == E_ARG
+    assert lib.nmp_ldasin_ingest(h, n, n, 0, _ptr(g), _ptr(pt), _ptr(blk), s) == E_ARG
+    assert lib.nmp_ldasin_ingest(h, n, n, 1 << 29, _ptr(g), _ptr(pt), _ptr(blk), s) == E_ARG
+    assert lib.nmp_ldasin_ingest(h, n, n, npts, None, _ptr(pt), _ptr(blk), s) == E_ARG
+    assert lib.nmp_ldasin_ingest(h, 0, n, npts, _ptr(g), _ptr(pt), _ptr(blk), s) == 0
+    assert lib.nmp_ldasout_grid(h, n, n, npts, L.NDIAG_FULL + 1, _ptr(diag), _ptr(pt), -9999.0,
+                                _ptr(out), s) == E_ARG
+    assert lib.nmp_ldasout_grid(h, n, n - 1, npts, 16, _ptr(diag), _ptr(pt), -9999.0, _ptr(out),
+                                s) == E_ARG
+    assert lib.nmp_ldasout_grid(h, n, n, npts, 16, None, _ptr(pt), -9999.0, _ptr(out), s) == E_ARG
+    assert lib.nmp_forcing_from_ldasin_geo(h, n, n, _ptr(blk), None, 0.0, 1.0, 0.0,
+                                           _ptr(diag), s) == E_ARG
+    torch.cuda.synchronize()
+    assert (blk == 7.0).all() and (out == 5).all()
+    eng.close()
