@@ -10,9 +10,13 @@ achieved HBM bandwidth against their algorithmic bytes, at 1,048,576 columns.
   ldasout_grid             fills 16 grids (64 B per grid point), then reads 16
                            fluxes + the point (68 B) and scatters them (64 B)
 
-Times are HIP events around `--reps` back-to-back launches on one stream
-(mean per launch); run under `rocprofv3 --kernel-trace --stats` for the
-kernels' own durations.  Prints one JSON line per kernel and precision.
+The two gather/scatter kernels are timed with the grid points in the
+columns' own order (`point` = identity: coalesced) and fully shuffled (every
+lane a different cache line: the worst case; the driver's coherent order lies
+between, mostly runs of neighbouring points).  Times are HIP events around
+`--reps` back-to-back launches on one stream (mean per launch); run under
+`rocprofv3 --kernel-trace --stats` for the kernels' own durations.  Prints
+one JSON line per kernel, precision and point order.
 
     python tools/io_kernels_bench.py [--ncol 1048576] [--reps 50]
 """
@@ -56,7 +60,8 @@ def main():
     n, dev = a.ncol, "cuda:0"
     rng = np.random.default_rng(0)
     npts = n
-    point = torch.as_tensor(rng.permutation(npts)[:n].astype(np.int32), device=dev)
+    points = {"identity": torch.arange(n, dtype=torch.int32, device=dev),
+              "shuffled": torch.as_tensor(rng.permutation(npts)[:n].astype(np.int32), device=dev)}
     lat = np.radians(rng.uniform(-60, 70, n))
     lon = np.radians(rng.uniform(-180, 180, n))
     geo = torch.as_tensor(np.stack([np.sin(lat), np.cos(lat), lon]), device=dev)
@@ -73,22 +78,26 @@ def main():
         grids = torch.empty((L.NDIAG_OUT, npts), device=dev,
                             dtype=torch.int32 if prec == 4 else torch.int64)
         cases = [
-            ("forcing_from_ldasin", lambda: eng.forcing_from_ldasin(blk, f),
+            ("forcing_from_ldasin", None, lambda: eng.forcing_from_ldasin(blk, f),
              n * (36 + 12 * prec)),
-            ("forcing_from_ldasin_geo", lambda: eng.forcing_from_ldasin(blk, f, geo=geo,
-                                                                        solar=solar),
+            ("forcing_from_ldasin_geo", None, lambda: eng.forcing_from_ldasin(blk, f, geo=geo,
+                                                                              solar=solar),
              n * (32 + 24 + 12 * prec)),
-            ("ldasout_grid", lambda: eng.ldasout_grid(diag, point, grids, -9999.0),
-             npts * 16 * prec + n * (16 * prec + 4 + 16 * prec)),
         ]
-        if prec == 4:
-            cases.append(("ldasin_ingest", lambda: eng.ldasin_ingest(grid_be, point, blk),
-                          n * (32 + 4 + 32)))
-        for name, fn, nbytes in cases:
+        for order, pt in points.items():
+            cases.append(("ldasout_grid", order,
+                          lambda pt=pt: eng.ldasout_grid(diag, pt, grids, -9999.0),
+                          npts * 16 * prec + n * (16 * prec + 4 + 16 * prec)))
+            if prec == 4:
+                cases.append(("ldasin_ingest", order,
+                              lambda pt=pt: eng.ldasin_ingest(grid_be, pt, blk),
+                              n * (32 + 4 + 32)))
+        for name, order, fn, nbytes in cases:
             ms = timed(fn, a.reps)
             gbs = nbytes / (ms * 1e-3) / 1e9
-            r = {"kernel": name, "precision": prec, "ncol": n, "ms_per_launch": ms,
-                 "algorithmic_bytes": nbytes, "achieved_gb_s": gbs, "hbm_frac": gbs / PEAK_GBS}
+            r = {"kernel": name, "precision": prec, "ncol": n, "point_order": order,
+                 "ms_per_launch": ms, "algorithmic_bytes": nbytes, "achieved_gb_s": gbs,
+                 "hbm_frac": gbs / PEAK_GBS}
             print(json.dumps(r), flush=True)
             out.append(r)
         eng.close()
