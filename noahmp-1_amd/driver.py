@@ -445,10 +445,11 @@ class OfflineDriver:
         """One output step's (16, n) fluxes, written on a background thread:
         on the current stream (after the step that produced them) the engine
         lays them on the file's grids in its byte order (nmp_ldasout_grid)
-        and they are copied into one of two pinned host buffers; the writer
-        thread waits for the copy and writes the header and the bytes
-        (ncio.write_ldasout_grids) while the loop goes on stepping.  A buffer
-        is reused once its previous file is written."""
+        and they are copied into the next of OUT_BUFFERS pinned host buffers;
+        a writer thread (OUT_WRITERS of them) waits for the copy and writes
+        the header and the bytes (ncio.write_ldasout_grids) while the loop
+        goes on stepping.  A buffer is reused once its previous file is
+        written."""
         src = d
         if self.grid is not None:
             if self._out_point is None:
@@ -465,7 +466,7 @@ class OfflineDriver:
             src = self._out_dev
         if self._writer is None:
             self._writer_init(tuple(src.shape), src.dtype)
-        k = self._n_out_w % 2
+        k = self._n_out_w % len(self._out_host)
         self._n_out_w += 1
         if self._out_fut[k] is not None:
             self._out_fut[k].result()
@@ -487,12 +488,17 @@ class OfflineDriver:
                          fields=np.array(",".join(L.DIAG_OUT)), diag=a)
         self._out_fut[k] = self._writer.submit(job)
 
+    # output files in flight at once (writer threads) and staging buffers: a
+    # file's write is a memory copy into the page cache on its own thread
+    OUT_WRITERS, OUT_BUFFERS = 2, 3
+
     def _writer_init(self, shape, dtype=None):
         from concurrent.futures import ThreadPoolExecutor
-        self._writer = ThreadPoolExecutor(1)
+        self._writer = ThreadPoolExecutor(self.OUT_WRITERS)
         dtype = dtype or self.dtype
-        self._out_host = [torch.empty(shape, dtype=dtype, pin_memory=True) for _ in range(2)]
-        self._out_fut, self._n_out_w = [None, None], 0
+        self._out_host = [torch.empty(shape, dtype=dtype, pin_memory=True)
+                          for _ in range(self.OUT_BUFFERS)]
+        self._out_fut, self._n_out_w = [None] * self.OUT_BUFFERS, 0
 
     def flush_output(self):
         """Wait until every output file issued so far is written (raises a
