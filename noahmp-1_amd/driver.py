@@ -92,17 +92,21 @@ class ForcingUpload:
         self.consumed = [()] * nbuf
         self.count = 0
 
-    def put(self, f: np.ndarray | None = None, fill=None) -> torch.Tensor:
+    def put(self, f: np.ndarray | None = None, fill=None, prefilled: bool = False) -> torch.Tensor:
         """Upload f, or whatever fill(host_array) writes into the pinned buffer
-        (a provider filling it in place saves a host copy)."""
+        (a provider filling it in place saves a host copy), or -- prefilled --
+        what a completed prefetch() left there."""
         b = self.count % len(self.host)
         self.count += 1
-        if self.uploaded[b] is not None:
-            self.uploaded[b].synchronize()  # pinned buffer b is free again
-        if fill is not None:
-            fill(self.host[b].numpy())
+        if prefilled:
+            pass  # prefetch() waited for the buffer's previous upload and filled it
         else:
-            self.host[b].numpy()[...] = f
+            if self.uploaded[b] is not None:
+                self.uploaded[b].synchronize()  # pinned buffer b is free again
+            if fill is not None:
+                fill(self.host[b].numpy())
+            else:
+                self.host[b].numpy()[...] = f
         for e in self.consumed[b]:
             self.stream.wait_event(e)
         with torch.cuda.stream(self.stream):
@@ -112,6 +116,19 @@ class ForcingUpload:
         self.uploaded[b], self.consumed[b] = ev, ()
         self._last = b
         return self.dev[b]
+
+    def prefetch(self, fill, executor):
+        """Fill the pinned buffer the next put() will use on `executor`, once
+        its previous upload has landed; the caller then calls put(prefilled=
+        True) after the returned future has completed without error."""
+        b = self.count % len(self.host)
+        ev, h = self.uploaded[b], self.host[b].numpy()
+
+        def job():
+            if ev is not None:
+                ev.synchronize()
+            fill(h)
+        return executor.submit(job)
 
     @property
     def last_slot(self) -> int:
@@ -223,6 +240,7 @@ class OfflineDriver:
             self.raw_fbuf = torch.empty((2, L.NFORCING, self.cs.ncol), dtype=self.dtype,
                                         device=self.dev)
         self.geo, self._raw_t, self._raw = None, None, None
+        self._prefetch, self._prefetch_pool = None, None
         if self.raw_upload is not None and cosz == "device":
             self.geo = torch.as_tensor(self.forcing.geo(), device=self.dev).contiguous()
         self.ingest = None
@@ -434,10 +452,23 @@ class OfflineDriver:
         if self.ingest is None or file_cosz or not self.forcing.ingestible(t):
             return self.raw_upload.put(fill=lambda h: self.forcing.block(t, out=h)), \
                 self.raw_upload
-        up = self.ingest
-        g = up.put(fill=lambda h: self.forcing.grid_raw(t, out=h))
+        up, ti = self.ingest, self.forcing.input_time(t)
+        ready = False
+        if self._prefetch is not None and self._prefetch[0] == ti:
+            # the file's bytes were read while the previous file's steps ran
+            ready = self._prefetch[1].exception() is None
+        self._prefetch = None
+        g = up.put(fill=lambda h: self.forcing.grid_raw(t, out=h), prefilled=ready)
         blk = self.ingest_blk[up.last_slot]
         self.engine.ldasin_ingest(g, self.point, blk, stream=up.stream)
+        # read the next input file's bytes ahead (a missing or non-fp32 file
+        # fails only the prefetch; its step then takes the plain path)
+        nxt = ti + self.forcing.every
+        if self._prefetch_pool is None:
+            from concurrent.futures import ThreadPoolExecutor
+            self._prefetch_pool = ThreadPoolExecutor(1)
+        self._prefetch = (nxt, up.prefetch(lambda h: self.forcing.grid_raw(nxt, out=h),
+                                           self._prefetch_pool))
         return blk, up
 
     # ---- output -----------------------------------------------------------------
