@@ -136,14 +136,15 @@ class ForcingUpload:
         caller keeps per slot are guarded by the same events)."""
         return self._last
 
-    def consumed_by(self, streams):
-        """The last put's device buffer is read by launches on `streams`."""
+    def consumed_by(self, streams, slot: int | None = None):
+        """The last put's device buffer (or slot `slot`'s) is read by launches
+        on `streams`."""
         evs = []
         for s in streams:
             e = torch.cuda.Event()
             e.record(s)
             evs.append(e)
-        self.consumed[self._last] = tuple(evs)
+        self.consumed[self._last if slot is None else slot] = tuple(evs)
 
 
 class DeviceSyntheticForcing:
@@ -239,8 +240,12 @@ class OfflineDriver:
                                             nfield=L.NLDASIN)
             self.raw_fbuf = torch.empty((2, L.NFORCING, self.cs.ncol), dtype=self.dtype,
                                         device=self.dev)
-        self.geo, self._raw_t, self._raw = None, None, None
+        self.geo, self._blocks = None, {}
         self._prefetch, self._prefetch_pool = None, None
+        # single-rank output: grids and copies on a stream of their own, so the
+        # next steps need not wait for them (only the next output step waits
+        # for the diagnostics buffer to be read: _diag_free)
+        self.out_stream, self._diag_free = None, None
         if self.raw_upload is not None and cosz == "device":
             self.geo = torch.as_tensor(self.forcing.geo(), device=self.dev).contiguous()
         self.ingest = None
@@ -361,7 +366,7 @@ class OfflineDriver:
             # restart copies, the gather fence assemble() left there) and, for
             # host forcing, for the upload of this step's buffer
             cur = torch.cuda.current_stream(self.dev)
-            pre, after, upload = None, (cur, self.upload.stream), self.upload
+            pre, after, upload, slot = None, (cur, self.upload.stream), self.upload, None
             tp = time.perf_counter()
             # the input file's variable names (header only, once per input time)
             info = self.forcing.variables(t0) if hasattr(self.forcing, "variables") else None
@@ -374,22 +379,27 @@ class OfflineDriver:
                 geo = solar = None
                 if self.geo is not None:
                     # the file's variables go up once per input interval and
-                    # stay resident; COSZ is formed on the device every step
+                    # stay resident; COSZ is formed on the device every step.
+                    # The ranges wait only for their own block's event, so the
+                    # next file's upload (enqueued as soon as its bytes are
+                    # read) runs beside the steps instead of before one.
                     ti = self.forcing.input_time(t0)
-                    if ti != self._raw_t:
-                        self._raw, self._raw_up = self._put_block(t_k, "COSZ" in info)
-                        self._raw_t = ti
-                    raw, upload = self._raw, self._raw_up
+                    if ti not in self._blocks:
+                        self._blocks[ti] = self._put_block(t_k, "COSZ" in info)
+                    for k in [k for k in self._blocks if k < ti]:
+                        del self._blocks[k]
+                    raw, ready, upload, slot = self._blocks[ti]
                     if "COSZ" not in info:
                         geo = self.geo
                         solar = timeman.solar_terms(timeman.julian(t0), timeman.yearlen(t0.year))
+                    after = (cur, ready)
                 else:
                     raw = self.raw_upload.put(fill=lambda h: self.forcing.raw(step_k, t_k, out=h))
                     upload = self.raw_upload
+                    after = (cur, upload.stream)
                 f = self.raw_fbuf[self.step_index % 2]
                 pre = lambda st, rng: self.engine.forcing_from_ldasin(  # noqa: E731
                     raw, f, stream=st, cols=rng, geo=geo, solar=solar)
-                after = (cur, upload.stream)
             elif self.dev_forcing is not None:
                 clim, fbuf = self.dev_forcing
                 f = fbuf[self.step_index % 2]
@@ -410,11 +420,16 @@ class OfflineDriver:
                 b = self.n_out % len(self.gather.bufs)
                 self.gather.release(b, self.ranges.streams)
                 diag = self.gather.local(b)
+            if out and self._diag_free is not None:
+                # the output stream's last read of the diagnostics buffer
+                after = (after if isinstance(after, tuple) else (after,)) + (self._diag_free,)
             self.ranges.step(f, self.zsoil, self.dt, timeman.julian(t0), timeman.yearlen(t0.year),
                              diag if out else None, L.DIAG_OUT_LEVEL if out else L.DIAG_NONE,
                              after=after, pre=pre)
             if upload is not None:
-                upload.consumed_by(self.ranges.producers)
+                upload.consumed_by(self.ranges.producers, slot)
+            if self.geo is not None and self.ingest is not None:
+                self._put_next_block(t0)
             self.phase_s["launch"] += time.perf_counter() - tp
             tp = time.perf_counter()
             self.t, self.step_index = t1, self.step_index + 1
@@ -423,14 +438,22 @@ class OfflineDriver:
                     self.gather.start(b, producers=self.ranges.producers)
                     d = self.gather.assemble(b)
                     self.n_out += 1
+                    ost = torch.cuda.current_stream(self.dev)
                 else:
-                    self.ranges.join()
+                    # single rank: the output's grids and copy run on their own
+                    # stream after this step, beside the next steps
+                    if self.out_stream is None:
+                        self.out_stream = torch.cuda.Stream(self.dev)
+                    ost = self.out_stream
+                    self.ranges.join(ost)
                     d = self.diag
                 if rank == 0:
                     os.makedirs(cfg.outdir, exist_ok=True)
                     path = (ncio.ldasout_path(cfg.outdir, t1) if self.grid is not None else
                             os.path.join(cfg.outdir, f"{_stamp(t1)}.LDASOUT.npz"))
-                    self._write_output(d, path, t1)
+                    freed = self._write_output(d, path, t1, ost)
+                    if self.gather is None:
+                        self._diag_free = freed
                     self.written.append(path)
             self.phase_s["output"] += time.perf_counter() - tp
             if _is_boundary(t1, cfg.begdatetime, res_every) and self.write:
@@ -450,8 +473,11 @@ class OfflineDriver:
         the engine forms the block's rows (nmp_ldasin_ingest on the upload's
         stream); otherwise the host builds the block (ncio block)."""
         if self.ingest is None or file_cosz or not self.forcing.ingestible(t):
-            return self.raw_upload.put(fill=lambda h: self.forcing.block(t, out=h)), \
-                self.raw_upload
+            up = self.raw_upload
+            blk = up.put(fill=lambda h: self.forcing.block(t, out=h))
+            ev = torch.cuda.Event()
+            ev.record(up.stream)
+            return blk, ev, up, up.last_slot
         up, ti = self.ingest, self.forcing.input_time(t)
         ready = False
         if self._prefetch is not None and self._prefetch[0] == ti:
@@ -469,18 +495,37 @@ class OfflineDriver:
             self._prefetch_pool = ThreadPoolExecutor(1)
         self._prefetch = (nxt, up.prefetch(lambda h: self.forcing.grid_raw(nxt, out=h),
                                            self._prefetch_pool))
-        return blk, up
+        ev = torch.cuda.Event()
+        ev.record(up.stream)
+        return blk, ev, up, up.last_slot
+
+    def _put_next_block(self, t: datetime.datetime):
+        """Once the next input file's bytes have been read ahead, upload and
+        ingest them (on the upload stream, beside the steps of this
+        interval) -- when that file takes the ingest path."""
+        pf = self._prefetch
+        if pf is None or pf[0] in self._blocks or not pf[1].done():
+            return
+        nxt = pf[0]
+        if pf[1].exception() is not None:
+            return  # the boundary step reads it itself (and raises if it must)
+        info = self.forcing.variables(nxt)
+        if {"CO2AIR", "O2AIR", "COSZ"} & info or not self.forcing.ingestible(nxt):
+            return
+        self._blocks[nxt] = self._put_block(nxt, False)
 
     # ---- output -----------------------------------------------------------------
-    def _write_output(self, d: torch.Tensor, path: str, t1: datetime.datetime):
+    def _write_output(self, d: torch.Tensor, path: str, t1: datetime.datetime, stream=None):
         """One output step's (16, n) fluxes, written on a background thread:
-        on the current stream (after the step that produced them) the engine
-        lays them on the file's grids in its byte order (nmp_ldasout_grid)
+        on `stream` (after the step that produced them) the engine lays them
+        on the file's grids in its byte order (nmp_ldasout_grid)
         and they are copied into the next of OUT_BUFFERS pinned host buffers;
         a writer thread (OUT_WRITERS of them) waits for the copy and writes
         the header and the bytes (ncio.write_ldasout_grids) while the loop
         goes on stepping.  A buffer is reused once its previous file is
-        written."""
+        written.  The device work goes on `stream` (default: the current
+        one); returns the event after which `d` has been read."""
+        stream = stream or torch.cuda.current_stream(self.dev)
         src = d
         if self.grid is not None:
             if self._out_point is None:
@@ -493,7 +538,7 @@ class OfflineDriver:
                                             dtype=torch.int32 if d.dtype == torch.float32
                                             else torch.int64)
             self.engine.ldasout_grid(d, self._out_point, self._out_dev, float(ncio.FILL),
-                                     stream=torch.cuda.current_stream(self.dev))
+                                     stream=stream)
             src = self._out_dev
         if self._writer is None:
             self._writer_init(tuple(src.shape), src.dtype)
@@ -504,9 +549,10 @@ class OfflineDriver:
         h = self._out_host[k]
         if h is None or h.shape != src.shape or h.dtype != src.dtype:
             h = self._out_host[k] = torch.empty(src.shape, dtype=src.dtype, pin_memory=True)
-        h.copy_(src, non_blocking=True)
-        ev = torch.cuda.Event()
-        ev.record(torch.cuda.current_stream(self.dev))
+        with torch.cuda.stream(stream):
+            h.copy_(src, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(stream)
 
         def job():
             ev.synchronize()
@@ -518,6 +564,7 @@ class OfflineDriver:
                 np.savez(path, time=np.array(t1.isoformat()),
                          fields=np.array(",".join(L.DIAG_OUT)), diag=a)
         self._out_fut[k] = self._writer.submit(job)
+        return ev
 
     # output files in flight at once (writer threads) and staging buffers: a
     # file's write is a memory copy into the page cache on its own thread

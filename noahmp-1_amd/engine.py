@@ -440,9 +440,9 @@ class StreamShards:
     def step(self, forcing: torch.Tensor, zsoil, dt: float, julian: float, yearlen: int,
              diag: torch.Tensor | None = None, diag_level: int = L.DIAG_NONE, events=None,
              after="current", pre=None):
-        """One step of every range.  `after`: the stream, or a tuple of streams,
-        whose pending work (the forcing upload, a previous reader of `diag`)
-        each range waits for first -- by default the caller's current stream,
+        """One step of every range.  `after`: the stream, or a tuple of streams
+        and events, whose pending work (the forcing upload, a previous reader
+        of `diag`) each range waits for first -- by default the caller's current stream,
         where torch enqueues uploads; tensors are kept alive until the ranges
         are done with them.  Pass None only when the inputs are known to be
         complete (e.g. after a synchronize).
@@ -456,7 +456,10 @@ class StreamShards:
         for i, (st, rng) in enumerate(zip(self.streams, self.ranges)):
             if after is not None:
                 for a in after:
-                    st.wait_stream(a)
+                    if isinstance(a, torch.cuda.Event):
+                        st.wait_event(a)
+                    else:
+                        st.wait_stream(a)
                 forcing.record_stream(st)
                 if diag is not None:
                     diag.record_stream(st)
