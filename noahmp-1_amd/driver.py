@@ -502,9 +502,12 @@ class OfflineDriver:
     def _put_next_block(self, t: datetime.datetime):
         """Once the next input file's bytes have been read ahead, upload and
         ingest them (on the upload stream, beside the steps of this
-        interval) -- when that file takes the ingest path."""
+        interval) -- when that file takes the ingest path.  Only the interval
+        right after t's: the one after that would take the slot this
+        interval's remaining steps still read (two slots)."""
         pf = self._prefetch
-        if pf is None or pf[0] in self._blocks or not pf[1].done():
+        if pf is None or pf[0] in self._blocks or not pf[1].done() or \
+                pf[0] != self.forcing.input_time(t) + self.forcing.every:
             return
         nxt = pf[0]
         if pf[1].exception() is not None:
