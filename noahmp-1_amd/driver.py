@@ -359,6 +359,7 @@ class OfflineDriver:
         for _ in range(total):
             if self.t >= cfg.enddatetime:
                 break
+            t_iter = time.perf_counter()
             t0 = self.t
             t1 = t0 + cfg.timestep
             out = _is_boundary(t1, cfg.begdatetime, out_every) and self.write
@@ -461,6 +462,7 @@ class OfflineDriver:
                 name = (f"RESTART.{_stamp(t1)}_DOMAIN1.nc" if self.grid is not None and
                         not dist.is_initialized() else f"RESTART.{_stamp(t1)}.r{rank}.npz")
                 self.save_restart(os.path.join(cfg.resdir, name))
+            self.phase_s["loop"] += time.perf_counter() - t_iter
         self.ranges.join()
         torch.cuda.synchronize(self.dev)
         self.flush_output()

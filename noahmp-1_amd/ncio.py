@@ -435,6 +435,9 @@ class LdasinForcing:
         """The variable names of the input file of t (its header only, cached
         per input time)."""
         ti = self.input_time(t)
+        cache = self.__dict__.setdefault("_vars_cache", {})
+        if ti in cache:
+            self._vars_t, (self._vars, self._ingestible) = ti, cache[ti]
         if getattr(self, "_vars_t", None) != ti:
             path = ldasin_path(self.indir, ti)
             if not os.path.isfile(path):
@@ -452,6 +455,9 @@ class LdasinForcing:
             finally:
                 f.close()
             self._vars_t = ti
+            cache[ti] = (self._vars, self._ingestible)
+            while len(cache) > 4:   # the current and next input times, a few back
+                del cache[min(cache)]
         return self._vars
 
     def ingestible(self, t: datetime.datetime) -> bool:
