@@ -351,7 +351,20 @@ class OfflineDriver:
             self.zsoil = [float(v) for v in z["zsoil"]]
 
     # ---- time loop -----------------------------------------------------------------
+    # the interpreter's thread switch interval while the loop runs: the file
+    # reader and writer threads hand the GIL back within this instead of 5 ms
+    SWITCH_INTERVAL_S = 0.0005
+
     def run(self, nsteps: int | None = None):
+        import sys
+        old = sys.getswitchinterval()
+        sys.setswitchinterval(min(old, self.SWITCH_INTERVAL_S))
+        try:
+            return self._run(nsteps)
+        finally:
+            sys.setswitchinterval(old)
+
+    def _run(self, nsteps: int | None = None):
         cfg = self.cfg
         total = cfg.step_count() if nsteps is None else nsteps
         rank = dist.get_rank() if dist.is_initialized() else 0

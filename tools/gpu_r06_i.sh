@@ -5,7 +5,7 @@
 set -u
 R="${GRAFT_REPO_ROOT:-/root/repo}"
 cd "$R"
-O=$R/gpurun_out/${TAG:-r06x}
+O=$R/gpurun_out/${TAG:-r06y}
 mkdir -p "$O"
 export PYTHONUNBUFFERED=1
 step() {  # name seconds cmd...
