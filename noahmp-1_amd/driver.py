@@ -334,6 +334,12 @@ class OfflineDriver:
 
     def load_restart(self, path: str):
         self.ranges.join()  # no range may still be stepping the state being replaced
+        # the resident LDASIN blocks and the read-ahead belong to the old time:
+        # a block kept across a jump could sit in a slot the next upload reuses
+        self._blocks.clear()
+        if self._prefetch is not None:
+            self._prefetch[1].exception()  # a running read-ahead finishes with its buffer
+        self._prefetch = None
         if path.endswith(".nc"):
             st, isn, self.t, self.step_index = ncio.read_state(path, self.grid,
                                                                self.cs.state.cpu().numpy().dtype)

@@ -429,3 +429,46 @@ def test_rccl_gather_path_on_one_gpu(engine_lib):
     res = json.loads(line[-1])
     print(res)
     assert r.returncode == 0 and res["ok"], res
+
+
+def test_driver_ingest_restart_jump_back(engine_lib, tmp_path):
+    """The device-ingest path across a restart loaded into the same driver:
+    run 60 steps of standard HRLDAS files (hourly, 4 steps per file: blocks
+    resident, the next file read ahead and uploaded beside the steps), load
+    the restart written at step 24 and run to the end again.  The final state
+    equals an uninterrupted run bit for bit: no block or read-ahead of the
+    later time survives the jump into a slot the earlier files reuse."""
+    from noahmp_amd import ncio
+    from test_config import write_case
+    from test_ncio import grid_for
+    g = load("traj_casenml.npz")
+    cols = _cols(g)
+    grid = grid_for(cols)
+    static, init, indir = tmp_path / "geo_em.d01.nc", tmp_path / "init.nc", tmp_path / "ldasin"
+    indir.mkdir()
+    nml = write_case(tmp_path)
+    text = open(nml).read().replace("'geo_em.d01.nc'", f"'{static}'").replace(
+        '"init.nc"', f'"{init}"').replace("'ldasin'", f"'{indir}'")
+    open(nml, "w").write(text)
+    cfg = config.Config(nml)
+    ncio.write_static(str(static), cols, grid)
+    ncio.write_state(str(init), grid, g["state0"], g["isnow0"], cfg.begdatetime)
+    t = cfg.begdatetime
+    for k in range(0, 96, 4):
+        ncio.write_ldasin(ncio.ldasin_path(str(indir), t), grid, g["forcing"][k], t, extras=False)
+        t = t + cfg.input_interval
+    ref = driver.OfflineDriver.from_files(cfg, write=False).run()
+    assert ref.ingest is not None and ref.ingest.count == 24
+    want = ref.cs.state.cpu().numpy()
+    ref.engine.close()
+    drv = driver.OfflineDriver.from_files(cfg, write=False)
+    drv.run(nsteps=24)
+    path = str(tmp_path / "mid.nc")
+    drv.save_restart(path)
+    drv.run(nsteps=36)                     # on to step 60, files read ahead
+    drv.load_restart(path)                 # back to step 24
+    assert drv.step_index == 24 and not drv._blocks
+    drv.run()
+    assert drv.step_index == 96
+    assert bit_equal(drv.cs.state.cpu().numpy(), want).all()
+    drv.engine.close()
