@@ -573,6 +573,9 @@ def ldasout_header(grid: Grid, kind: str, t: datetime.datetime) -> bytes:
         metas.append([_nc_name(name), i4(3), i4(0), i4(1), i4(2), i4(12), i4(1),
                       _nc_name("_FillValue"), i4(nc_type), i4(1), fill, i4(nc_type), i4(vsize)])
     size = sum(len(x) for x in h) + sum(sum(len(x) for x in m) + 4 for m in metas)
+    if size + len(metas) * vsize > 2**31 - 1:  # CDF-1 offsets are signed 32-bit
+        raise ValueError(f"LDASOUT of {ny} x {nx} {kind} grids exceeds the classic format's "
+                         "2 GiB offsets")
     for i, m in enumerate(metas):
         h += m + [i4(size + i * vsize)]         # begin (32-bit offsets, version 1)
     return b"".join(h)
