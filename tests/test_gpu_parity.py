@@ -1166,29 +1166,33 @@ def test_midloop_domain_exit_bit_exact():
     assert r.returncode == 0 and res["ok"], res
 
 
-def test_full_size_year_sample_vs_reference(engines):
-    """Config #5's grid in fp32 for a whole hourly year on the product path:
-    1,036,800 global columns, opt_veg 2 (carbon on), 8,784 steps of 3,600 s
-    through the bench's two stream ranges, the forcing generated on the device
-    before each range's launch (nmp_forcing_synth), the 16 output fluxes every
-    step.  512 seeded columns are re-run through the reference Fortran itself
-    (oracle/_ref: ref_sflx_run, the time loop in the harness, JULIAN formed
-    there as julian0 + s*dt/86400 in default real) with the forcing the device
-    generated for them: their state and ISNOW after each of 12 chunks of 732
-    steps, and each chunk's last output fluxes, equal the reference's bit for
-    bit.  The year test at 256 columns covers the physics; this one the launch
-    at BASELINE size for as long as config #5 runs."""
+@pytest.mark.parametrize("cfg", ["cfg5", "cfg3"])
+def test_full_size_year_sample_vs_reference(engines, cfg):
+    """A whole year on the product path at BASELINE size, in fp32: config #5's
+    grid (1,036,800 global columns, opt_veg 2: carbon on, 8,784 steps of
+    3,600 s) or config #3's set (1,048,576 mixed columns, opt_veg 1, 17,568
+    steps of 1,800 s), through the bench's two stream ranges, the forcing
+    generated on the device before each range's launch (nmp_forcing_synth),
+    the 16 output fluxes every step.  512 seeded columns are re-run through
+    the reference Fortran itself (oracle/_ref: ref_sflx_run, the time loop in
+    the harness, JULIAN formed there as julian0 + s*dt/86400 in default real)
+    with the forcing the device generated for them: their state and ISNOW
+    after each of 12 chunks, and each chunk's last output fluxes, equal the
+    reference's bit for bit.  The year tests at 256 columns cover the physics;
+    this one the launch at BASELINE size for a whole year."""
     import ref
     from noahmp_amd.engine import ColumnState, StreamShards
     from noahmp_amd.params import Params
     if not ref.available():
         pytest.skip("reference oracle not built (oracle/_ref)")
     P = Params.builtin()
-    opts = dict(L.CASE_NML_OPTIONS, opt_veg=2)
+    kind, opt_veg, n, dt, nsteps = {"cfg5": ("global", 2, 1_036_800, 3600.0, 8784),
+                                    "cfg3": ("mixed", 1, 1_048_576, 1800.0, 17568)}[cfg]
+    opts = dict(L.CASE_NML_OPTIONS, opt_veg=opt_veg)
     otuple = tuple(opts[k] for k in L.OPTION_NAMES)
     eng = engines(otuple, 4)
-    n, dt, nsteps, nchunk, yl, seed = 1_036_800, 3600.0, 8784, 12, 366, 5
-    cols = cases.make_columns(n, "global", P.as_dict(), seed=seed, julian=0.0)
+    nchunk, yl, seed = 12, 366, 5
+    cols = cases.make_columns(n, kind, P.as_dict(), seed=seed, julian=0.0)
     idx = np.sort(np.random.default_rng(seed).choice(n, 512, replace=False))
     cs = ColumnState.from_host(cols, DEV, torch.float32)
     clim = torch.as_tensor(cases.climate(cols), device=DEV).float().contiguous()
