@@ -484,7 +484,6 @@ def main():
                     tj.get("order", "as-generated") == a.order and \
                     (a.order == "as-generated" or tj.get("order_band", 4.0) == a.order_band) and \
                     tj.get("out_every", 2) == a.out_every and \
-                    tj.get("vege_cap", 0) == 0 and \
                     tj.get("source_hash") == _build.source_hash() \
                     and os.environ.get("NOAHMP_ENGINE_LIB") is None:
                 traffic = tj.get("bytes_per_launch")

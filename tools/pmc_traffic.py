@@ -84,7 +84,7 @@ def main():
             if ln.startswith("{") and '"build_hash"' in ln:
                 measured = json.loads(ln)["checks"]["build_hash"]
     res = {"source_hash": measured or build.source_hash(), "ncol": ncol, "streams": streams, "kind": kind,
-           "out_every": out_every, "order": order, "vege_cap": 0,
+           "out_every": out_every, "order": order,
            "precision": 4, "math": "ref", "kernel": KERNEL, "dispatches": nb,
            "fetch_size_kb": bf, "write_size_kb": bw, "read_correction": rf,
            "write_correction": rw, "read_bytes": rd, "write_bytes": wr,
