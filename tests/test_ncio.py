@@ -204,3 +204,13 @@ def test_ldasout_from_grids_is_the_same_file(tmp_path, ref_params):
             ncio.write_ldasout_grids(b, grid, full, t)
             assert open(a, "rb").read() == open(b, "rb").read()
             assert np.array_equal(bits(ncio.read_ldasout(b, grid)), bits(diag))
+
+
+def test_ldasout_header_refuses_past_classic_offsets():
+    """A grid whose 16 fp64 fluxes pass the classic format's signed 32-bit
+    offsets (2 GiB) is refused rather than written with wrapped offsets."""
+    big = ncio.Grid(np.zeros((1, 1)), np.zeros((1, 1)), np.ones((1, 1), bool))
+    big.shape = (4096, 4096)          # 16.8 M points: 16 x 8 B x 16.8 M = 2.1 GB
+    with pytest.raises(ValueError, match="2 GiB"):
+        ncio.ldasout_header(big, "f8", T0)
+    assert len(ncio.ldasout_header(big, "f4", T0)) > 0   # 1.07 GB fits
