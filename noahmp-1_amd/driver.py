@@ -30,19 +30,24 @@ allowed), which writes them for the whole grid.
 
 Forcing reaches the GPU through `ForcingUpload`: pinned, double-buffered
 host buffers copied on a copy stream, so the host builds step t+1's forcing
-while the GPU steps t.  From LDASIN files (cosz="device", the default) the
-upload is a file's 8 variables, once per input interval (ncio.LdasinForcing
-.block, 32 B per column per file), which stay resident while the engine forms
-the 12 forcing fields, COSZ included, on each range's stream right before its
-launch (nmp_forcing_from_ldasin_geo): no host work and no upload on the steps
-between files.  cosz="host" uploads the variables plus the host's COSZ every
-step (ncio.LdasinForcing.raw, 36 B per column, nmp_forcing_from_ldasin); the
-12-field host form (48 B per column, 96 in fp64) remains for providers that
-supply all of them.
+while the GPU steps t.  From LDASIN files (cosz="device", ingest=True, the
+defaults) a file's bytes go up as stored, once per input interval
+(ncio.LdasinForcing.grid_raw, read ahead on a thread), and the engine forms
+the block in its column order (nmp_ldasin_ingest) on the upload stream,
+beside the steps of the previous file; the block stays resident while each
+range forms the 12 forcing fields, COSZ included, on its own stream right
+before its launch (nmp_forcing_from_ldasin_geo), waiting only on that
+block's event.  ingest=False builds the block on the host
+(ncio.LdasinForcing.block); cosz="host" uploads the variables plus the
+host's COSZ every step (ncio.LdasinForcing.raw, nmp_forcing_from_ldasin);
+the 12-field host form (48 B per column, 96 in fp64) remains for providers
+that supply all of them.  A single rank's output is laid on the file's grids
+(nmp_ldasout_grid) and copied on a stream of its own and written by writer
+threads (ncio.write_ldasout_grids).
 
-`phase_s` accumulates the host time of the loop's parts (forcing provider,
-upload enqueue, launch enqueue, output), for the offline-driver timing
-(tools/offline_timing.py).
+`phase_s` accumulates the host time of the loop's parts (file headers,
+forcing, launch enqueue, output hand-off, the whole iteration), for the
+offline-driver timing (tools/offline_timing.py).
 """
 from __future__ import annotations
 
