@@ -224,6 +224,18 @@ def test_timeman():
     c_noon = timeman.cosz(lat, np.array([0.0]), 172.5, 366)
     c_night = timeman.cosz(lat, np.array([0.0]), 172.0, 366)
     assert c_noon[0] > 0.9 and c_night[0] < 0
+    # cosz is solar_terms' factors combined in one fixed order (the device's
+    # nmp_forcing_from_ldasin_geo takes the same factors): restated, bit for bit
+    import math
+    rng = np.random.default_rng(4)
+    la, lo = np.radians(rng.uniform(-90, 90, 4096)), np.radians(rng.uniform(-180, 180, 4096))
+    for jul in (0.0, 80.0, 172.3125, 365.9583):
+        sd, cd, ha0 = timeman.solar_terms(jul, 366)
+        decl = 0.409 * math.sin(2.0 * math.pi * (jul - 80.0) / 366)
+        assert (sd, cd) == (math.sin(decl), math.cos(decl))
+        assert ha0 == 2.0 * math.pi * (((jul - math.floor(jul)) * 24.0) / 24.0)
+        want = np.sin(la) * sd + (np.cos(la) * cd) * np.cos((ha0 + lo) - math.pi)
+        assert np.array_equal(timeman.cosz(la, lo, jul, 366).view(np.int64), want.view(np.int64))
 
 
 @pytest.mark.parametrize("kind", ["casenml", "mixed", "conus"])
