@@ -17,7 +17,7 @@ export NOAHMP_ENGINE_LIB="$R/noahmp-1_amd/lib/variants/lib_trunc.so"
 P1="SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY"
 P2="SQ_INSTS_VALU_ADD_F32 SQ_INSTS_VALU_MUL_F32 SQ_INSTS_VALU_FMA_F32 SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_FMA_F64 SQ_WAVES"
 P3="SQ_INSTS_SALU SQ_INSTS_VALU_INT32 SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS SQ_INSTS_BRANCH SQ_WAIT_ANY SQ_WAVES"
-BENCH="$R/bench.py --steps 4 --warmup 1 --period 4 --no-cpu-baseline"
+BENCH="$R/bench.py --steps 4 --warmup 1 --period 4 --no-cpu-baseline ${BENCH_ARGS:-}"
 for k in ${MARKS:-2 3 4 5 6 14 9 10 11 13 99}; do
   export NMP_TRUNC_AT=$k
   mkdir -p "$OUT/m$k"
