@@ -17,6 +17,7 @@ transcendental, f64, int32, other), SALU / branch / LDS / VMEM counts, and the
 wait share (SQ_WAIT_INST_ANY / SQ_WAVE_CYCLES).
 
     python tools/phase_counters.py gpurun_out/<tag> [--out profiles/r06/phase_counters.json]
+                                   [--label "config #5 fp64"]
 """
 import csv
 import glob
@@ -109,8 +110,9 @@ def main():
     for p in phases:
         p["time_share"] = p["kernel_ms"] / tot_ms
         p["weighted_valu_share"] = p["weighted_valu_cycles_per_wave"] / tot_w
+    label = sys.argv[sys.argv.index("--label") + 1] if "--label" in sys.argv else "config #3"
     out = {"source": f"tools/phase_counters.sh truncation runs ({base}); lib_trunc.so "
-                     "(-DNMP_TRUNC_RUNTIME), config #3 bench, 4 steps after 1",
+                     f"(-DNMP_TRUNC_RUNTIME), {label} bench, 4 steps after 1",
            "cumulative": {str(k): cum[k] for k in marks}, "phases": phases}
     print(f"{'phase':42s} {'ms':>7s} {'time%':>6s} {'VALU/wave':>9s} {'lane':>5s} "
           f"{'f32':>6s} {'f64':>6s} {'trans':>6s} {'other':>6s} {'wait%':>6s}")
