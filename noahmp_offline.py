@@ -42,17 +42,28 @@ def main(argv=None):
     ap.add_argument("--device-forcing", action="store_true",
                     help="synthetic cases: generate the forcing on the GPU every step "
                          "(nmp_forcing_synth) instead of on the host")
+    ap.add_argument("--precision", type=int, default=4, choices=(4, 8),
+                    help="engine precision (fp32, the reference's, or fp64)")
+    ap.add_argument("--cosz", default="device", choices=("device", "host"),
+                    help="netCDF cases: COSZ formed on the device from the grid (default) or "
+                         "computed on the host and uploaded every step")
+    ap.add_argument("--no-ingest", action="store_true",
+                    help="netCDF cases: build each LDASIN block on the host instead of "
+                         "uploading the file's bytes for the device to select and order")
     a = ap.parse_args(argv)
     cfg = config.Config(a.nmlfile)
     P = Params.builtin()
     if os.path.isfile(cfg.constfile):
-        drv = driver.OfflineDriver.from_files(cfg, device=a.device, params=P, init=a.restart)
+        drv = driver.OfflineDriver.from_files(cfg, device=a.device, params=P, init=a.restart,
+                                              precision=a.precision, cosz=a.cosz,
+                                              ingest=not a.no_ingest)
         a.ncol = drv.cs.ncol
     else:
         cols = cases.make_columns(a.ncol, a.kind, P.as_dict(), seed=0,
                                   julian=timeman.julian(cfg.begdatetime))
         drv = driver.OfflineDriver(cfg, cols, device=a.device, params=P,
-                                   forcing="device" if a.device_forcing else None)
+                                   forcing="device" if a.device_forcing else None,
+                                   precision=a.precision)
         if a.restart:
             drv.load_restart(a.restart)
     t0 = time.perf_counter()
