@@ -1034,6 +1034,15 @@ static __device__ unsigned int nmp_fb_reason[32];
 #ifndef NMP_SOIL_DIV
 #define NMP_SOIL_DIV 1
 #endif
+// NMP_VD_CHECKED: bit 0 the canopy loop's CTR, TR and DTV, bit 1 the bare
+// loop's DTG also divide with DivFast32, their numerators checked per lane
+// every iteration (vege_domain.h NUM_LO_EXP / NUM_HI_EXP; outside: the lane
+// re-runs its loop with IEEE division).  Both on: config #3 +0.4 to +1.4 %
+// interleaved on two boxes, neither alone measurable
+// (profiles/r06/ab/vd_checked_ab.txt)
+#ifndef NMP_VD_CHECKED
+#define NMP_VD_CHECKED 3
+#endif
 #ifndef NMP_VEGE_UNROLL
 #define NMP_VEGE_UNROLL 1
 #endif
@@ -1517,6 +1526,9 @@ DEV void sflx_column(const DevParams& P, const KArgs<T>& A, Col<T>& c, const Sin
       NMP_DOM(k, 12, in(fveg, NMP_DOM_FVEG_LO, 1.0));
       NMP_DOM(k, 13, in(sqrt_dleaf_uc, NMP_DOM_SDL_LO, NMP_DOM_SDL_HI));
       NMP_DOM(k, 14, in(rsurf, 0.0, NMP_DOM_RSURF_HI));
+#if NMP_VD_CHECKED & 1
+      NMP_DOM(k, 15, in(emg, 0.0, 1.0));  // bounds DTV's denominator A
+#endif
 #ifdef NMP_VD_NODOMAIN
       k = true;  // (timing probe only: not exact in general)
 #endif
@@ -1527,11 +1539,12 @@ DEV void sflx_column(const DevParams& P, const KArgs<T>& A, Col<T>& c, const Sin
     // lane can run it again with the reference's divisions.
     auto vege_loop = [&](auto& d) -> bool {
       constexpr bool kFast = !std::is_same<std::decay_t<decltype(d)>, DivRef<T>>::value;
-      // CTR, TR and DTV keep IEEE division under every policy: their
-      // numerators are products of several possibly small factors, outside
-      // what the range proof bounds (tools/div_proof.py)
-#ifdef NMP_VD_ALLFAST
-      auto& dref = d;  // (timing probe only: not exact in general)
+      // CTR, TR and DTV: their numerators are products of several possibly
+      // small factors, outside what the range proof bounds statically
+      // (tools/div_proof.py).  IEEE division, or with NMP_VD_CHECKED the
+      // loop's policy and a per-lane window on each numerator (`nwin`).
+#if defined(NMP_VD_ALLFAST) || (NMP_VD_CHECKED & 1)
+      auto& dref = d;  // (NMP_VD_ALLFAST: timing probe only, not exact in general)
 #else
       const DivRef<T> dref;
 #endif
@@ -1540,6 +1553,11 @@ DEV void sflx_column(const DevParams& P, const KArgs<T>& A, Col<T>& c, const Sin
       // the first iteration; any miss sends the lane through the IEEE loop
       bool ok = true;
       auto in = [](T x, T lo, T hi) { return x >= lo && x <= hi; };
+      [[maybe_unused]] auto nwin = [](T x) {
+        const T ax = fabs(x);
+        return (x == L(0.0)) | ((ax >= (T)__builtin_ldexp(1.0, NMP_DOM_NUM_LO_EXP)) &
+                                (ax <= (T)__builtin_ldexp(1.0, NMP_DOM_NUM_HI_EXP)));
+      };
       cmv = c.cm;
       chv = c.ch;
       fv = L(0.1); h = L(0.0); hg = L(0.0);
@@ -1651,16 +1669,27 @@ DEV void sflx_column(const DevParams& P, const KArgs<T>& A, Col<T>& c, const Sin
         T aea = d.div(eair * caw + estg * cgw, rcond2);
         T bea = d.div(cew + ctw, rcond2);
         T cev = d.div((L(1.0) - bea) * cew * rhoair * CPAIR, rgammav);
-        T ctr = dref.div((L(1.0) - bea) * ctw * rhoair * CPAIR, rgammav);
+        const T ctr_n = (L(1.0) - bea) * ctw * rhoair * CPAIR;
+#if NMP_VD_CHECKED & 1
+        if constexpr (kFast) NMP_DOM(ok, 26, nwin(ctr_n));
+#endif
+        T ctr = dref.div(ctr_n, rgammav);
         c.tah = ata + bta * c.tv;
         c.eah = aea + bea * estv;
         irc = fveg * (air + cir * p4(c.tv));
         shc = fveg * rhoair * CPAIR * cvh * (c.tv - c.tah);
         evc = d.div(fveg * rhoair * CPAIR * cew * (estv - c.eah), rgammav);
-        tr = dref.div(fveg * rhoair * CPAIR * ctw * (estv - c.eah), rgammav);
+        const T tr_n = fveg * rhoair * CPAIR * ctw * (estv - c.eah);
+#if NMP_VD_CHECKED & 1
+        if constexpr (kFast) NMP_DOM(ok, 27, nwin(tr_n));
+#endif
+        tr = dref.div(tr_n, rgammav);
         evc = rmin((c.tv > TFRZ) ? evlim_liq : evlim_ice, evc);
         T b = sav - irc - shc - evc - tr;
         T a = fveg * (L(4.0) * cir * p3(c.tv) + csh + (cev + ctr) * destv);
+#if NMP_VD_CHECKED & 1
+        if constexpr (kFast) NMP_DOM(ok, 28, nwin(b));
+#endif
         T dtv = dref.div(b, dref.rec(a));
         irc = irc + fveg * L(4.0) * cir * p3(c.tv) * dtv;
         shc = shc + fveg * csh * dtv;
@@ -1701,8 +1730,8 @@ DEV void sflx_column(const DevParams& P, const KArgs<T>& A, Col<T>& c, const Sin
 #endif
 #ifdef NMP_COUNT_FALLBACK
         atomicAdd(&nmp_fallback_ctr, 1u);
-        for (int b = 0; b < 20; ++b)
-          if (fb_why & (1u << b)) atomicAdd(&nmp_fb_reason[b], 1u);
+        for (int b = 0; b < 29; ++b)
+          if ((0x1c0fffffu >> b) & (fb_why >> b) & 1u) atomicAdd(&nmp_fb_reason[b], 1u);
 #endif
         c.tv = out.ls(NMP_S_TV);
         c.tah = out.ls(NMP_S_TAH);
@@ -1781,12 +1810,22 @@ NMP_UNROLL(NMP_LOOP2_UNROLL)
     // The bare-ground Newton loop (func.f90:3120-3200) with the division
     // policy `d`, as the canopy loop: every loop variable starts here, so a
     // lane outside the range proof's domain can run it again with IEEE
-    // division.  DTG = B/A keeps IEEE division under every policy.
+    // division.  DTG = B/A: IEEE division, or with NMP_VD_CHECKED & 2 the
+    // loop's policy and a per-lane window on B.
     auto bare_loop = [&](auto& d) -> bool {
       constexpr bool kFast = !std::is_same<std::decay_t<decltype(d)>, DivRef<T>>::value;
+#if NMP_VD_CHECKED & 2
+      auto& dref = d;
+#else
       const DivRef<T> dref;
+#endif
       bool ok = true;
       auto in = [](T x, T lo, T hi) { return x >= lo && x <= hi; };
+      [[maybe_unused]] auto nwin = [](T x) {
+        const T ax = fabs(x);
+        return (x == L(0.0)) | ((ax >= (T)__builtin_ldexp(1.0, NMP_DOM_NUM_LO_EXP)) &
+                                (ax <= (T)__builtin_ldexp(1.0, NMP_DOM_NUM_HI_EXP)));
+      };
       tgb = c.tg;
       cmb = c.cm;
       chb = c.ch;
@@ -1825,6 +1864,9 @@ NMP_UNROLL(NMP_BARE_UNROLL)
         ghb = cgh * (tgb - stc_top);
         T b = sag - irb - shb - evb - ghb;
         T a = L(4.0) * cir * p3(tgb) + csh + cev * destg + cgh;
+#if NMP_VD_CHECKED & 2
+        if constexpr (kFast) NMP_DOM(ok, 29, nwin(b));
+#endif
         T dtg = dref.div(b, dref.rec(a));
         irb = irb + L(4.0) * cir * p3(tgb) * dtg;
         shb = shb + csh * dtg;
@@ -1852,6 +1894,9 @@ NMP_UNROLL(NMP_BARE_UNROLL)
                          in(lgb.tmpch2, NMP_DOM_TMPC_LO, NMP_DOM_TMPC_HI));
       NMP_DOM(k, 23, in(zlvl - zpdg, NMP_DOM_DZ_LO, NMP_DOM_DZ_HI) &
                          in(z0mg, NMP_DOM_Z0_LO, NMP_DOM_Z0_HI) & in(rsurf, 0.0, NMP_DOM_RSURF_HI));
+#if NMP_VD_CHECKED & 2
+      NMP_DOM(k, 30, in(emg, 0.0, 1.0) & in(cgh, 0.0, NMP_DOM_CGH_HI));  // DTG's A
+#endif
 #ifdef NMP_VD_NODOMAIN
       k = true;
 #endif
@@ -1864,8 +1909,8 @@ NMP_UNROLL(NMP_BARE_UNROLL)
       if (!bare_domain_ok() || !bare_loop(dfb)) {
 #ifdef NMP_COUNT_FALLBACK
         atomicAdd(&nmp_fallback_ctr, 1u);
-        for (int b = 20; b < 24; ++b)
-          if (fb_why & (1u << b)) atomicAdd(&nmp_fb_reason[b], 1u);
+        for (int b = 20; b < 31; ++b)
+          if ((0x60f00000u >> b) & (fb_why >> b) & 1u) atomicAdd(&nmp_fb_reason[b], 1u);
 #endif
         bare_loop(drb);
       }

@@ -124,6 +124,22 @@
 #ifndef NMP_DOM_TGB_HI
 #define NMP_DOM_TGB_HI NMP_DOM_T_HI
 #endif
+// The numerators of CTR, TR and DTV = B/A (canopy loop) and DTG = B/A (bare
+// loop) are products and sums of several possibly small terms that no static
+// bound keeps away from the subnormals; with NMP_VD_CHECKED they are checked
+// per lane every iteration instead: 0, or 2^NUM_LO_EXP <= |x| <= 2^NUM_HI_EXP
+// (a lane outside re-runs its loop with IEEE division).  The ground emissivity
+// EMG lies in [0, 1] and the bare loop's CGH = 2*DF/DZ of the top layer in
+// [0, CGH_HI], both checked once per column: they bound the denominators A.
+#ifndef NMP_DOM_NUM_LO_EXP
+#define NMP_DOM_NUM_LO_EXP -96
+#endif
+#ifndef NMP_DOM_NUM_HI_EXP
+#define NMP_DOM_NUM_HI_EXP 64
+#endif
+#ifndef NMP_DOM_CGH_HI
+#define NMP_DOM_CGH_HI 1.0e6
+#endif
 
 // ---- the stomata bisection (stomata, func.f90:3739-3887; sflx_kernel.hip
 // stomata_solve), run in the canopy loop's first iteration.  Its six divisions

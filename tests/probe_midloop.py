@@ -2,7 +2,9 @@
 
 The probe library (`lib_probe_midloop.so`, built by __graft_entry__.build()
 from the shipped sources with the per-iteration windows narrowed:
-NMP_DOM_TV_HI / NMP_DOM_TGB_HI / NMP_DOM_RAHG_HI, plus NMP_COUNT_FALLBACK)
+NMP_DOM_TV_HI / NMP_DOM_TGB_HI / NMP_DOM_RAHG_HI, and the numerator windows of
+CTR / TR / DTV / DTG raised to |x| >= 4 (NMP_DOM_NUM_LO_EXP=2), plus
+NMP_COUNT_FALLBACK)
 sends many lanes out of the range proof's domain PART WAY through the canopy
 and bare Newton loops, after the fast loop has changed TV/TAH/EAH, QSFC and
 the first iteration's stomata outputs.  Those lanes re-run the loop with IEEE
@@ -38,7 +40,8 @@ import port  # noqa: E402  (the oracle: the checker)
 
 # fb_why bits (sflx_kernel.hip NMP_DOM): the windows checked inside the loops
 IN_LOOP = {16: "RAHG window", 17: "RSSUN/RSSHA", 19: "TV window (iter >= 2)",
-           20: "TGB window (bare)"}
+           20: "TGB window (bare)", 26: "CTR numerator", 27: "TR numerator",
+           28: "DTV numerator", 29: "DTG numerator (bare)"}
 
 
 def main():
@@ -83,7 +86,8 @@ def main():
                        "in_loop": {IN_LOOP[b]: int(why[b]) for b in IN_LOOP},
                        "columns_differing": int((~ok).sum())}
                 res["runs"].append(run)
-                ok_all = ok_all and bool(ok.all() and fb > 0 and why[19] > 0 and why[20] > 0)
+                ok_all = ok_all and bool(ok.all() and fb > 0 and why[19] > 0 and why[20] > 0
+                                         and why[28] > 0 and why[29] > 0)
     # soil water (NMP_SOIL_DIV): very dry clay (SOILTYP 12, BEXP 11.55) makes
     # WDF * DDZ fall below 2^-102, outside DivFast32's exact region: those
     # divisions must take IEEE division (fb_reason[25]) and every column keep

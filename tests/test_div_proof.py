@@ -14,6 +14,8 @@ def test_every_short_division_site_is_inside_the_exact_region():
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
     assert "sites inside the exact region" in r.stdout
     assert r.stdout.count("stomata:") >= 7, "stomata bisection sites missing from the proof"
+    for s in ("CTR = ", "TR = ", "DTV = B / A", "bare: DTG = B / A"):
+        assert s in r.stdout, f"{s} missing from the proof"
 
 
 def test_shipped_vegetation_tables_inside_the_stomata_box():

@@ -101,6 +101,12 @@ VARIANTS = {
     "vdnowin": {"f32": ["-DNMP_VD_NOWIN"]},
     "vdallfast": {"f32": ["-DNMP_VD_ALLFAST"]},
     "vdnone": {"f32": ["-DNMP_VD_NODOMAIN", "-DNMP_VD_NOWIN", "-DNMP_VD_ALLFAST"]},
+    # round 6: CTR, TR, DTV (bit 0) and bare DTG (bit 1) on DivFast32 with
+    # per-lane numerator windows (exact: a lane outside re-runs with IEEE)
+    "vdchk": {"f32": ["-DNMP_VD_CHECKED=3"]},
+    "vdchk1": {"f32": ["-DNMP_VD_CHECKED=1"]},
+    "vdchk2": {"f32": ["-DNMP_VD_CHECKED=2"]},
+    "vdchk_fb": {"f32": ["-DNMP_VD_CHECKED=3", "-DNMP_COUNT_FALLBACK"]},
     "nopeel": ("-DNMP_VEGE_NOPEEL",),
     "vu2": ("-DNMP_VEGE_UNROLL=2",),
     "vu3": ("-DNMP_VEGE_UNROLL=3",),

@@ -348,7 +348,7 @@ def main():
     bea = site("BEA = (CEW+CTW) / COND", M(min(cew.lo, ctw.lo), cew.hi + ctw.hi, True), cond2,
                ":2832", "FWET = 0: CTW = the LAI terms; FWET > 0: >= CEW")
     one_m_bea = M(2.0 ** -24, 1.0, True)            # BEA <= 1; 1 - BEA is 0 or >= 2^-24
-    site("CEV = (1-BEA)*CEW*RHOAIR*CPAIR / GAMMAV", one_m_bea * cew * rhocp, gammav, ":2833")
+    cev = site("CEV = (1-BEA)*CEW*RHOAIR*CPAIR / GAMMAV", one_m_bea * cew * rhocp, gammav, ":2833")
     # EAH = AEA + BEA*ESTV lies between 0 and max(EAIR, ESTG, ESTV); ESTV >= es.lo, so
     # ESTV - EAH is 0 or >= 2^(E - 23) with E the exponent of es.lo / 2
     de = M(2.0 ** (math.floor(math.log2(es.lo / 2)) - 23), max(es.hi, eair_hi), True)
@@ -359,6 +359,22 @@ def main():
     hg_q = site("HG = RHOAIR*CPAIR*(TG-TAH) / RAHG", rhocp * dT, rahg, ":2865")
     site("QSFC = 0.622*EAH / (SFCPRS-0.378*EAH)", 0.622 * eah,
          M(p.lo - 0.378 * eah.hi, p.hi), ":2868")
+    # ---- CTR, TR, DTV = B/A (NMP_VD_CHECKED): the numerators are checked per
+    # lane every iteration (vege_domain.h NUM_LO_EXP / NUM_HI_EXP); the
+    # denominators are bounded here.  A = FVEG*(4*CIR*TV**3 + CSH + (CEV+CTR)*DESTV),
+    # every term >= 0: CIR = (2 - EMV*(1-EMG))*EMV*SB with EMG in [0, 1] (checked)
+    # and EMV = 1 - EXP(-VAI), VAI = VAIE*FVEG >= VAI_LO*FVEG_LO; CSH =
+    # (1-BTA)*RHOAIR*CPAIR*CVH <= RHOAIR*CPAIR*CVH; CTR <= RHOAIR*CPAIR*CTW / GAMMAV. ----
+    numw = M(2.0 ** D["NUM_LO_EXP"] * (1 + 2 * W), 2.0 ** D["NUM_HI_EXP"], True)
+    note = "numerator window checked per lane, IEEE loop outside"
+    site("CTR = (1-BEA)*CTW*RHOAIR*CPAIR / GAMMAV", numw, gammav, ":2834", note)
+    site("TR = FVEG*RHOAIR*CPAIR*CTW*(ESTV-EAH) / GAMMAV", numw, gammav, ":2843", note)
+    emv = M(-math.expm1(-D["VAI_LO"] * D["FVEG_LO"]) * 0.9, 1.0)  # fp32 rounding of 1 - EXP(-x) near 1: < 6e-8
+    cir = M(emv.lo * SB, 2 * SB)
+    ctr_hi = rhocp.hi * ctw.hi / gammav.lo
+    a_v = M(fveg.lo * 4 * cir.lo * T.lo ** 3,
+            4 * cir.hi * T.hi ** 3 + rhocp.hi * cvh.hi + (cev.hi + ctr_hi) * des.hi)
+    site("DTV = B / A", numw, a_v, ":2852", note)
     # ---- bare_flux's Newton loop (:3120-3200; sflx_kernel.hip bare_loop) ----
     # Same sfcdif1 sites with Z0H = Z0MG and ZPD = ZPDG (the snow depth): the
     # kernel checks the same limits on TMPCM.., ZLVL-ZPDG, Z0MG, SFCTMP, air,
@@ -373,7 +389,12 @@ def main():
     site("bare: CSH = RHOAIR*CPAIR / RAHB", rhocp, rahb, ":3186")
     gammag = gammav                                  # same formula with LATHEAG
     cevi = site("bare: RHOAIR*CPAIR / GAMMA", rhocp, gammag, ":3187")
-    site("bare: CEV = (...) / (RSURF+RAWB)", cevi, M(rahb.lo, rahb.hi + rsurf_hi), ":3187")
+    cevb = site("bare: CEV = (...) / (RSURF+RAWB)", cevi, M(rahb.lo, rahb.hi + rsurf_hi), ":3187")
+    # A = 4*CIR*TGB**3 + CSH + CEV*DESTG + CGH, every term >= 0 (CIR = EMG*SB,
+    # EMG in [0, 1] and CGH in [0, CGH_HI] checked per column): >= CSH
+    a_b = M(rhocp.lo / rahb.hi,
+            4 * SB * T.hi ** 3 + rhocp.hi / rahb.lo + cevb.hi * des.hi + D["CGH_HI"])
+    site("bare: DTG = B / A", numw, a_b, ":3198", note)
 
     stomata_sites(D, T, p, es, rb)
     soil_sites()
@@ -391,9 +412,6 @@ def main():
     for name, ref, a, b, q, ok, note in rows:
         print(f"{name:46s} {ref:8s} {a!r:>22s} {b!r:>22s} {q!r:>22s}  {'yes' if ok else 'NO'}"
               + (f"  ({note})" if note else ""))
-    print("IEEE kept (not in the table): CTR :2834, TR :2843, DTV = B/A :2852, bare DTG = B/A "
-          ":3198 -- their numerators are sums or products of several possibly small terms "
-          "whose bound falls below 2^-102")
     print(f"derived: FHG >= {fhg_lo:.3g}, CWPC in {cwpc!r}, FV in {fv!r}, RAHC in {rahc!r}, "
           f"RB in {rb!r}")
     if bad:

@@ -33,7 +33,10 @@ def main():
                  9: "VAIE", 10: "LAISUNE/LAISHAE", 11: "FWET", 12: "FVEG", 13: "SQRT(DLEAF/UC)",
                  14: "RSURF", 16: "RAHG window", 17: "RSSUN/RSSHA", 18: "TV at entry",
                  19: "TV window", 20: "TGB window (bare)", 21: "bare: air/pressure/wind",
-                 22: "bare: TMPCM..", 23: "bare: heights/RSURF"}
+                 22: "bare: TMPCM..", 23: "bare: heights/RSURF", 24: "stomata on IEEE",
+                 25: "soil-water division on IEEE", 15: "EMG", 26: "CTR numerator",
+                 27: "TR numerator", 28: "DTV numerator", 29: "bare: DTG numerator",
+                 30: "bare: EMG/CGH"}
     for kind, n, opt_veg, nsteps in (("mixed", 1 << 20, 1, 25), ("conus", 1 << 20, 1, 25),
                                      ("global", 1_036_800, 2, 25), ("casenml", 65536, 1, 96)):
         eng = Engine(P, dict(L.CASE_NML_OPTIONS, opt_veg=opt_veg), device=0)

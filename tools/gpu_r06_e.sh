@@ -30,8 +30,10 @@ fi
 cd /tmp && export TMPDIR=/tmp
 step ktrace 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/ktrace" -o run -- python3 "$R/bench.py" --steps 20 --warmup 5 --no-cpu-baseline
 cd "$R"
-step bench_with_traffic 300 python -u bench.py --steps 20 --warmup 5 --no-cpu-baseline
-step bench_48 300 python -u bench.py --no-cpu-baseline
+TR=()
+[ -f "$O/traffic.json" ] && TR=(--traffic "$O/traffic.json")  # this build's PMC passes
+step bench_with_traffic 300 python -u bench.py --steps 20 --warmup 5 --no-cpu-baseline "${TR[@]}"
+step bench_48 300 python -u bench.py "${TR[@]}"
 if [ "${CONFIGS:-1}" = 1 ]; then
   TAG=${TAG:-r06e}/configs step configs 900 bash tools/configs.sh
 fi
